@@ -1,0 +1,195 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X NTT polynomial multiplier (BASELINE.json metric).
+
+One "step" = one batched product c = a * b mod (x^n + 1, q) over this rank's shard of
+synthetic polynomials already resident in HBM (generated on the device from the counter-based
+splitmix64 stream of SURVEY §8d, so every rank owns a contiguous slice [p0, p0 + batch) of one
+global batch and no input crosses PCIe or xGMI).  Scaling is weak: each GPU multiplies
+--batch-per-gpu polynomials per step; shards are independent, there is no collective on the data
+path (torch.distributed only provides the barrier and the max-over-ranks time).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 4096] [--q 2013265921]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Prints ONE JSON line on rank 0 (fields documented in DESIGN.md §Measurement).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ntt-based-polynomial-multiplier-fpga_amd"))
+
+METRIC = "polymults/sec (n=4096, 32-bit q) at 1/2/4/8 MI355X; % HBM roofline"
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+SEED = 0x4E54544D554C
+
+
+def shard(global_batch: int, rank: int, world: int):
+    """Contiguous slice [p0, p1) of the global batch owned by `rank`."""
+    p0 = global_batch * rank // world
+    p1 = global_batch * (rank + 1) // world
+    return p0, p1
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n", type=int, default=4096)
+    ap.add_argument("--q", type=int, default=2013265921)
+    ap.add_argument("--batch-per-gpu", type=int, default=65536)
+    ap.add_argument("--word-bits", type=int, default=0, help="32/64 coefficient storage (0: auto)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="target wall time of the CPU-baseline sample")
+    return ap.parse_args(argv)
+
+
+def cpu_baseline(n: int, q: int, target_s: float):
+    """The oracle's psi-merged lazy-Shoup port of the reference's optimized path (oracle/), OpenMP
+    over the batch on this host's cores; bounded sample sized to ~target_s seconds."""
+    import numpy as np
+    from oracle import oracle as O
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or O.num_threads()
+    P = O.Plan(n, q)
+    if q >= (1 << 31):
+        return None
+    per = max(64, threads * 16)
+    a, b = O.fill_inputs(n, q, 0, per)
+    a = a.astype(np.uint32)
+    b = b.astype(np.uint32)
+    _, t = P.fast_batch_u32(a, b, threads)              # warm + calibrate
+    reps = max(1, int(target_s / max(t, 1e-6)))
+    total_t = 0.0
+    for _ in range(reps):
+        _, t = P.fast_batch_u32(a, b, threads)
+        total_t += t
+    return {"value": per * reps / total_t, "unit": "polymults/s", "cores": threads, "kind": "port",
+            "sample": f"{per * reps} polymults (n={n}, q={q}) = {reps} passes over {per} "
+                      f"counter-based inputs, OpenMP {threads} threads, "
+                      f"{total_t:.1f} s, oracle/nttmul_oracle.c orc_fast_batch_u32"}
+
+
+def load_traffic(n: int, q: int, batch: int):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), if one matches."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        data = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    for e in data.get("entries", []):
+        if e.get("n") == n and e.get("q") == q and e.get("batch") == batch:
+            return e.get("hbm_bytes_per_launch")
+    return None
+
+
+def main(argv=None):
+    args = parse(argv)
+    import torch
+    import torch.distributed as dist
+    import nttmul
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    n, q = args.n, args.q
+    wb = args.word_bits or (32 if q < (1 << 32) else 64)
+    batch = args.batch_per_gpu
+    global_batch = batch * world
+    p0, p1 = shard(global_batch, rank, world)
+
+    ctx = nttmul.Context(n, q, ndev=1, first_dev=local)
+    dt = torch.int32 if wb == 32 else torch.int64
+    a = torch.empty((p1 - p0) * n, dtype=dt, device=dev)
+    b = torch.empty_like(a)
+    c = torch.empty_like(a)
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+    ctx.fill_random_device(a, b, p0, p1 - p0, wb, seed=SEED, stream=sptr)
+
+    def step():
+        ctx.multiply_device(c, a, b, p1 - p0, wb, stream=sptr)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1) / args.steps   # HIP events on the launch stream
+
+    wall_t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
+    wall_max = float(wall_t.item())
+
+    if rank == 0:
+        value = global_batch * args.steps / wall_max
+        wbytes = wb // 8
+        alg_bytes = 3 * n * wbytes * (p1 - p0)           # read a, b + write c, per launch
+        achieved = alg_bytes / (kern_ms * 1e-3) / 1e9     # GB/s
+        single_launch = n <= 4096
+        traffic = load_traffic(n, q, batch)
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "polymults/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": wall_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32" if wb == 32 else "u64",
+            "data": "synthetic: splitmix64 counter-based coefficients mod q, generated on device "
+                    "(SURVEY §8d, seed 0x4E54544D554C)",
+            "config": {"workload": f"C3: n={n}, q={q}, batch {batch} polymults per GPU "
+                                   f"(global {global_batch}), device-resident",
+                       "n": n, "q": q, "batch_per_gpu": batch, "global_batch": global_batch,
+                       "parallelism": f"batch shards x{world}, no collective"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "k_rows<Arith32,u32,u32,12,0>" if (single_launch and wb == 32)
+                         else "polymul (all launches of one step)",
+                         "kernel_ms": kern_ms,
+                         "alg_bytes_per_launch": alg_bytes},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                line["cpu_baseline"] = cpu_baseline(n, q, args.cpu_seconds)
+            except Exception as e:  # the baseline is reported, never required
+                line["cpu_baseline"] = {"error": str(e)}
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,442 @@
+// kernels.hip — gfx950 kernels of the negacyclic polynomial product c = a * b mod (x^n + 1, q).
+//
+// Algorithm (reference = NTT_Software/NTT_Software_Evaluations/NTT-256/NTT/ntt.C):
+//   forward  : mulntt_ct_std2rev (ntt.C:342-371) — psi-merged Cooley-Tukey, standard order in,
+//              bit-reversed out, twiddle p[t+j] = psi^(n/2t) omega^((n/2t) bitrev(j))
+//   pointwise: mul_array (ntt.C:131-137) in the bit-reversed domain (order-agnostic)
+//   inverse  : nttmul_gs_rev2std (ntt.C:428-451) — psi^-1-merged Gentleman-Sande, bit-reversed
+//              in, standard out; the n^-1 of ntt256.C:12 is folded into the last stage
+// Every butterfly of forward-stage index st (t = 2^st, distance d = n >> (st+1)) acting on lower
+// element e uses twiddle index 2^st + (e >> (logn - st)) in both directions (the inverse runs the
+// same stages in reverse order).  No bit-reversal permutation is ever materialised.
+//
+// Kernel shapes
+//   k_rows   : fused per polynomial (n <= 4096): 256-thread block, 16 coefficients per thread,
+//              stages in register groups of <= 4 (radix-16), LDS transposes between groups,
+//              a and b transformed together (shared twiddle loads), pointwise, inverse, store.
+//              For n > 4096 the same kernel is the "row" pass of a two-level decomposition
+//              n = 2^L1 * 2^LOGS: rows are contiguous 2^LOGS-blocks whose stages are the last LOGS.
+//   k_cols_* : the first L1 <= 4 stages for n > 4096 (column pass), one column per thread in
+//              registers, lanes on consecutive columns (coalesced), no LDS.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "launch.hpp"
+#include "modarith.hpp"
+
+namespace nttmul {
+
+template <class A>
+struct KParams {
+  A ar;
+  const TwPair<typename A::word> *fw;  // forward twiddles  (mixed_powers_rev + Shoup)
+  const TwPair<typename A::word> *iw;  // inverse twiddles  (inv_mixed_powers_rev + Shoup)
+  typename A::word f, fs;              // F  = n^-1 R mod q (R = Montgomery radix)
+  typename A::word wf, wfs;            // iw[1] * F mod q
+};
+
+// ---------------------------------------------------------------------------------------------
+// Layout algebra of the register groups (all compile-time except the per-thread base)
+// ---------------------------------------------------------------------------------------------
+template <int LOGS>
+struct Groups {
+  static constexpr int N = 1 << LOGS;
+  static constexpr int G = (LOGS + 3) / 4;
+  static constexpr int S(int g) { return LOGS / G + (g < LOGS % G ? 1 : 0); }
+  static constexpr int ST0(int g) {
+    int s = 0;
+    for (int i = 0; i < g; i++) s += S(i);
+    return s;
+  }
+  static constexpr int NS(int g) { return 16 >> S(g); }         // independent sets per thread
+  static constexpr int LR(int g) { return LOGS - ST0(g) - S(g); } // log2 of the group's min distance
+  static constexpr int LNS(int g) { return 4 - S(g); }
+  // element index = base(g, j) + off(g, k), with base and off bit-disjoint (so the LDS pad
+  // e + (e >> 4) also splits into a per-thread part and an immediate offset).
+  static constexpr int off(int g, int k) {
+    int ns = NS(g), lr = LR(g), s = S(g);
+    int m = k / ns, sidx = k % ns;
+    if (lr >= LNS(g)) return sidx + (m << lr);
+    return ((sidx >> lr) << (lr + s)) + (sidx & ((1 << lr) - 1)) + (m << lr);
+  }
+  __device__ static __forceinline__ int base(int g, int j) {
+    int lr = LR(g), s = S(g), lns = LNS(g);
+    if (lr >= lns) {
+      int set0 = j << lns;
+      return ((set0 >> lr) << (lr + s)) + (set0 & ((1 << lr) - 1));
+    }
+    return j << 4;
+  }
+  // block index of register k's set (twiddle index contribution), B = set >> lr
+  __device__ static __forceinline__ int blk(int g, int j, int k) {
+    int lr = LR(g), lns = LNS(g);
+    int sidx = k % NS(g);
+    if (g == 0) return 0;
+    if (lr >= lns) return (j << lns) >> lr;
+    return (j << (lns - lr)) + (sidx >> lr);
+  }
+  static constexpr int pad(int e) { return e + (e >> 4); }
+  static constexpr int NP = N + N / 16;  // padded LDS words per polynomial
+};
+
+template <class W, class T>
+__device__ __forceinline__ W to_word(T v) { return (W)v; }
+
+// Forward CT stages of group g on two polynomials (same twiddles).
+template <class A, int LOGS, int g>
+__device__ __forceinline__ void fwd_group(const A &ar, typename A::word (&x)[16],
+                                          typename A::word (&y)[16],
+                                          const TwPair<typename A::word> *__restrict__ tw, int j,
+                                          int row, int l1) {
+  using Gr = Groups<LOGS>;
+  constexpr int S = Gr::S(g), st0 = Gr::ST0(g), ns = Gr::NS(g);
+#pragma unroll
+  for (int l = 0; l < S; l++) {
+    const int dist = 8 >> l;
+    const int st = st0 + l;
+    const int tbase = (1 << (l1 + st)) + (row << st);
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      if (k & dist) continue;
+      const int m = k / ns;
+      const int idx = tbase + (Gr::blk(g, j, k) << l) + (m >> (S - l));
+      const TwPair<typename A::word> t = tw[idx];
+      ar.ct(x[k], x[k + dist], t.w, t.ws);
+      ar.ct(y[k], y[k + dist], t.w, t.ws);
+    }
+  }
+}
+
+// Inverse GS stages of group g (reverse stage order).  SCALE: fold F into the global stage 0.
+template <class A, int LOGS, int g, bool SCALE>
+__device__ __forceinline__ void inv_group(const KParams<A> &P, typename A::word (&x)[16],
+                                          const TwPair<typename A::word> *__restrict__ tw, int j,
+                                          int row, int l1) {
+  using Gr = Groups<LOGS>;
+  constexpr int S = Gr::S(g), st0 = Gr::ST0(g), ns = Gr::NS(g);
+#pragma unroll
+  for (int l = S - 1; l >= 0; l--) {
+    const int dist = 8 >> l;
+    const int st = st0 + l;
+    const int tbase = (1 << (l1 + st)) + (row << st);
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      if (k & dist) continue;
+      if (SCALE && st == 0) {
+        P.ar.gs_scaled(x[k], x[k + dist], P.f, P.fs, P.wf, P.wfs);
+      } else {
+        const int m = k / ns;
+        const int idx = tbase + (Gr::blk(g, j, k) << l) + (m >> (S - l));
+        const TwPair<typename A::word> t = tw[idx];
+        P.ar.gs(x[k], x[k + dist], t.w, t.ws);
+      }
+    }
+  }
+}
+
+// Move 16 registers of each region from layout gfrom to layout gto through LDS.
+template <int LOGS, int gfrom, int gto, int NREG, class W>
+__device__ __forceinline__ void exchange(W (&x)[16], W (&y)[16], W *lds_x, W *lds_y, int j) {
+  using Gr = Groups<LOGS>;
+  const int bw = Gr::pad(Gr::base(gfrom, j));
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    lds_x[bw + Gr::pad(Gr::off(gfrom, k))] = x[k];
+    if (NREG == 2) lds_y[bw + Gr::pad(Gr::off(gfrom, k))] = y[k];
+  }
+  __syncthreads();
+  const int br = Gr::pad(Gr::base(gto, j));
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    x[k] = lds_x[br + Gr::pad(Gr::off(gto, k))];
+    if (NREG == 2) y[k] = lds_y[br + Gr::pad(Gr::off(gto, k))];
+  }
+  __syncthreads();
+}
+
+template <class A, int LOGS, int g>
+__device__ __forceinline__ void fwd_all(const A &ar, typename A::word (&x)[16],
+                                        typename A::word (&y)[16], typename A::word *lx,
+                                        typename A::word *ly,
+                                        const TwPair<typename A::word> *__restrict__ tw, int j,
+                                        int row, int l1) {
+  using Gr = Groups<LOGS>;
+  fwd_group<A, LOGS, g>(ar, x, y, tw, j, row, l1);
+  if constexpr (g + 1 < Gr::G) {
+    exchange<LOGS, g, g + 1, 2>(x, y, lx, ly, j);
+    fwd_all<A, LOGS, g + 1>(ar, x, y, lx, ly, tw, j, row, l1);
+  }
+}
+
+template <class A, int LOGS, int g, bool SCALE>
+__device__ __forceinline__ void inv_all(const KParams<A> &P, typename A::word (&x)[16],
+                                        typename A::word (&y)[16], typename A::word *lx,
+                                        typename A::word *ly,
+                                        const TwPair<typename A::word> *__restrict__ tw, int j,
+                                        int row, int l1) {
+  inv_group<A, LOGS, g, SCALE>(P, x, tw, j, row, l1);
+  if constexpr (g > 0) {
+    exchange<LOGS, g, g - 1, 1>(x, y, lx, ly, j);
+    inv_all<A, LOGS, g - 1, SCALE>(P, x, y, lx, ly, tw, j, row, l1);
+  }
+}
+
+// Fused product of `units` independent rows of 2^LOGS coefficients.
+//   L1 == 0 : each unit is a whole polynomial (n = 2^LOGS): full product, canonical output.
+//   L1 >  0 : unit u is row (u mod 2^L1) of polynomial (u >> L1) after the column pass; the
+//             row's stages are global stages L1 .. L1+LOGS-1; output stays lazy in [0, 2q).
+template <class A, class TIn, class TOut, int LOGS, int L1>
+__global__ __launch_bounds__(256) void k_rows(KParams<A> P, const TIn *__restrict__ a,
+                                              const TIn *__restrict__ b, TOut *__restrict__ c,
+                                              size_t units) {
+  using W = typename A::word;
+  using Gr = Groups<LOGS>;
+  constexpr int N = Gr::N, TP = N / 16, PB = 256 / TP, G = Gr::G, NP = Gr::NP;
+  __shared__ W lds[PB][2][NP];
+
+  const int pb = threadIdx.x / TP, j = threadIdx.x % TP;
+  const size_t u = (size_t)blockIdx.x * PB + pb;
+  const bool live = u < units;
+  const int row = L1 ? (int)(u & ((1u << L1) - 1)) : 0;
+  const size_t base_g = u * N + Gr::base(0, j);
+
+  W x[16], y[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    x[k] = live ? to_word<W>(a[base_g + Gr::off(0, k)]) : W(0);
+    y[k] = live ? to_word<W>(b[base_g + Gr::off(0, k)]) : W(0);
+  }
+  W *lx = lds[pb][0], *ly = lds[pb][1];
+  fwd_all<A, LOGS, 0>(P.ar, x, y, lx, ly, P.fw, j, row, L1);
+#pragma unroll
+  for (int k = 0; k < 16; k++) x[k] = P.ar.mont(x[k], y[k]);
+  inv_all<A, LOGS, G - 1, L1 == 0>(P, x, y, lx, ly, P.iw, j, row, L1);
+  if (live) {
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      W v = x[k];
+      if (L1 == 0) v = P.ar.canon(v);
+      c[base_g + Gr::off(0, k)] = (TOut)v;
+    }
+  }
+}
+
+// Column pass, forward: global stages 0..L1-1 of CT on a and b.  Thread = one column
+// (e = col + m * 2^LOGS, m < 2^L1); lanes on consecutive columns -> coalesced rows.
+template <class A, class TIn, int L1>
+__global__ __launch_bounds__(256) void k_cols_fwd(KParams<A> P, const TIn *__restrict__ a,
+                                                  const TIn *__restrict__ b,
+                                                  typename A::word *__restrict__ ta,
+                                                  typename A::word *__restrict__ tb, size_t batch,
+                                                  int logs) {
+  using W = typename A::word;
+  constexpr int M = 1 << L1;
+  const size_t ncol = (size_t)1 << logs;
+  const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= batch * ncol) return;
+  const size_t p = gid >> logs, col = gid & (ncol - 1);
+  const size_t base = (p << (logs + L1)) + col;
+  W x[M], y[M];
+#pragma unroll
+  for (int m = 0; m < M; m++) {
+    x[m] = (W)a[base + ((size_t)m << logs)];
+    y[m] = (W)b[base + ((size_t)m << logs)];
+  }
+#pragma unroll
+  for (int st = 0; st < L1; st++) {
+    const int dist = M >> (st + 1);
+#pragma unroll
+    for (int m = 0; m < M; m++) {
+      if (m & dist) continue;
+      const TwPair<W> t = P.fw[(1 << st) + (m >> (L1 - st))];
+      P.ar.ct(x[m], x[m + dist], t.w, t.ws);
+      P.ar.ct(y[m], y[m + dist], t.w, t.ws);
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < M; m++) {
+    ta[base + ((size_t)m << logs)] = x[m];
+    tb[base + ((size_t)m << logs)] = y[m];
+  }
+}
+
+// Column pass, inverse: global stages L1-1..0 of GS, F folded into stage 0, canonical output.
+template <class A, class TOut, int L1>
+__global__ __launch_bounds__(256) void k_cols_inv(KParams<A> P,
+                                                  const typename A::word *__restrict__ tc,
+                                                  TOut *__restrict__ c, size_t batch, int logs) {
+  using W = typename A::word;
+  constexpr int M = 1 << L1;
+  const size_t ncol = (size_t)1 << logs;
+  const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= batch * ncol) return;
+  const size_t p = gid >> logs, col = gid & (ncol - 1);
+  const size_t base = (p << (logs + L1)) + col;
+  W x[M];
+#pragma unroll
+  for (int m = 0; m < M; m++) x[m] = tc[base + ((size_t)m << logs)];
+#pragma unroll
+  for (int st = L1 - 1; st >= 0; st--) {
+    const int dist = M >> (st + 1);
+#pragma unroll
+    for (int m = 0; m < M; m++) {
+      if (m & dist) continue;
+      if (st == 0) {
+        P.ar.gs_scaled(x[m], x[m + dist], P.f, P.fs, P.wf, P.wfs);
+      } else {
+        const TwPair<W> t = P.iw[(1 << st) + (m >> (L1 - st))];
+        P.ar.gs(x[m], x[m + dist], t.w, t.ws);
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < M; m++) c[base + ((size_t)m << logs)] = (TOut)P.ar.canon(x[m]);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Synthetic inputs and input validation
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+template <class T>
+__global__ void k_fill(T *a, T *b, uint32_t logn, uint64_t q, uint64_t seed, uint64_t p0,
+                       size_t total) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const uint64_t n = 1ull << logn;
+  const uint64_t p = i >> logn, k = i & (n - 1);
+  const uint64_t base = seed + 2ull * n * (p0 + p);
+  a[i] = (T)(splitmix64(base + k) % q);
+  b[i] = (T)(splitmix64(base + n + k) % q);
+}
+
+template <class T>
+__global__ void k_check_range(const T *a, const T *b, uint64_t q, size_t total, int *bad) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  if ((uint64_t)a[i] >= q || (uint64_t)b[i] >= q) atomicOr(bad, 1);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Host-side launchers (called from nttmul.cpp)
+// ---------------------------------------------------------------------------------------------
+template <class A>
+static KParams<A> make_params(const LaunchTables &T) {
+  using W = typename A::word;
+  KParams<A> P;
+  P.ar.q = (W)T.q;
+  P.ar.qinv_neg = (W)T.qinv_neg;
+  P.fw = (const TwPair<W> *)T.fw;
+  P.iw = (const TwPair<W> *)T.iw;
+  P.f = (W)T.f; P.fs = (W)T.fs; P.wf = (W)T.wf; P.wfs = (W)T.wfs;
+  return P;
+}
+
+template <class A, class TIn, class TOut, int LOGS, int L1>
+static hipError_t launch_rows(const KParams<A> &P, const void *a, const void *b, void *c,
+                              size_t units, hipStream_t s) {
+  constexpr int PB = 256 / ((1 << LOGS) / 16);
+  const size_t blocks = (units + PB - 1) / PB;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL((k_rows<A, TIn, TOut, LOGS, L1>), dim3((unsigned)blocks), dim3(256), 0, s, P,
+                     (const TIn *)a, (const TIn *)b, (TOut *)c, units);
+  return hipGetLastError();
+}
+
+// Fused single-launch product, n = 2^logn <= 4096.
+template <class A, class IO>
+static hipError_t fused(const LaunchTables &T, const void *a, const void *b, void *c,
+                        size_t batch, hipStream_t s) {
+  const KParams<A> P = make_params<A>(T);
+  switch (T.logn) {
+    case 8: return launch_rows<A, IO, IO, 8, 0>(P, a, b, c, batch, s);
+    case 9: return launch_rows<A, IO, IO, 9, 0>(P, a, b, c, batch, s);
+    case 10: return launch_rows<A, IO, IO, 10, 0>(P, a, b, c, batch, s);
+    case 11: return launch_rows<A, IO, IO, 11, 0>(P, a, b, c, batch, s);
+    case 12: return launch_rows<A, IO, IO, 12, 0>(P, a, b, c, batch, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// Multi-pass product, n = 2^logn in (4096, 65536]: rows of 4096, L1 = logn - 12 column stages.
+template <class A, class IO, int L1>
+static hipError_t multipass_l1(const LaunchTables &T, const void *a, const void *b, void *c,
+                               size_t batch, void *ta, void *tb, void *tc, hipStream_t s) {
+  using W = typename A::word;
+  const KParams<A> P = make_params<A>(T);
+  constexpr int LOGS = 12;
+  const size_t cols = batch << LOGS;
+  const unsigned cblocks = (unsigned)((cols + 255) / 256);
+  hipLaunchKernelGGL((k_cols_fwd<A, IO, L1>), dim3(cblocks), dim3(256), 0, s, P, (const IO *)a,
+                     (const IO *)b, (W *)ta, (W *)tb, batch, LOGS);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  e = launch_rows<A, W, W, LOGS, L1>(P, ta, tb, tc, batch << L1, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((k_cols_inv<A, IO, L1>), dim3(cblocks), dim3(256), 0, s, P,
+                     (const W *)tc, (IO *)c, batch, LOGS);
+  return hipGetLastError();
+}
+
+template <class A, class IO>
+static hipError_t multipass(const LaunchTables &T, const void *a, const void *b, void *c,
+                            size_t batch, void **scr, hipStream_t s) {
+  switch (T.logn) {
+    case 13: return multipass_l1<A, IO, 1>(T, a, b, c, batch, scr[0], scr[1], scr[2], s);
+    case 14: return multipass_l1<A, IO, 2>(T, a, b, c, batch, scr[0], scr[1], scr[2], s);
+    case 15: return multipass_l1<A, IO, 3>(T, a, b, c, batch, scr[0], scr[1], scr[2], s);
+    case 16: return multipass_l1<A, IO, 4>(T, a, b, c, batch, scr[0], scr[1], scr[2], s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_polymul(const LaunchTables &T, const void *a, const void *b, void *c,
+                          size_t batch, int io_bits, void **scr, hipStream_t s) {
+  const bool big = T.logn > 12;
+  if (T.word_bits == 32) {
+    if (io_bits == 64)  // 64-bit storage of a q < 2^31 product: same 32-bit arithmetic
+      return big ? multipass<Arith32, uint64_t>(T, a, b, c, batch, scr, s)
+                 : fused<Arith32, uint64_t>(T, a, b, c, batch, s);
+    return big ? multipass<Arith32, uint32_t>(T, a, b, c, batch, scr, s)
+               : fused<Arith32, uint32_t>(T, a, b, c, batch, s);
+  }
+  if (io_bits == 32)
+    return big ? multipass<Arith64, uint32_t>(T, a, b, c, batch, scr, s)
+               : fused<Arith64, uint32_t>(T, a, b, c, batch, s);
+  return big ? multipass<Arith64, uint64_t>(T, a, b, c, batch, scr, s)
+             : fused<Arith64, uint64_t>(T, a, b, c, batch, s);
+}
+
+hipError_t launch_fill(void *a, void *b, uint32_t logn, uint64_t q, uint64_t seed, uint64_t p0,
+                       size_t count, int io_bits, hipStream_t s) {
+  const size_t total = count << logn;
+  if (!total) return hipSuccess;
+  const unsigned blocks = (unsigned)((total + 255) / 256);
+  if (io_bits == 32)
+    hipLaunchKernelGGL(k_fill<uint32_t>, dim3(blocks), dim3(256), 0, s, (uint32_t *)a,
+                       (uint32_t *)b, logn, q, seed, p0, total);
+  else
+    hipLaunchKernelGGL(k_fill<uint64_t>, dim3(blocks), dim3(256), 0, s, (uint64_t *)a,
+                       (uint64_t *)b, logn, q, seed, p0, total);
+  return hipGetLastError();
+}
+
+hipError_t launch_check_range(const void *a, const void *b, uint64_t q, size_t total, int io_bits,
+                              int *bad, hipStream_t s) {
+  if (!total) return hipSuccess;
+  const unsigned blocks = (unsigned)((total + 255) / 256);
+  if (io_bits == 32)
+    hipLaunchKernelGGL(k_check_range<uint32_t>, dim3(blocks), dim3(256), 0, s,
+                       (const uint32_t *)a, (const uint32_t *)b, q, total, bad);
+  else
+    hipLaunchKernelGGL(k_check_range<uint64_t>, dim3(blocks), dim3(256), 0, s,
+                       (const uint64_t *)a, (const uint64_t *)b, q, total, bad);
+  return hipGetLastError();
+}
+
+}  // namespace nttmul

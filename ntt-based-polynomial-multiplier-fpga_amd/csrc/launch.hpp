@@ -1,0 +1,27 @@
+// launch.hpp — internal interface between the host runtime (nttmul.cpp) and the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace nttmul {
+
+// Per-device view of a plan: what a launch needs (pointers are device memory).
+struct LaunchTables {
+  uint32_t logn;
+  int word_bits;           // 32 -> Arith32 (q < 2^31), 64 -> Arith64
+  uint64_t q, qinv_neg;    // -q^-1 mod 2^word_bits
+  uint64_t f, fs, wf, wfs; // F = n^-1 R mod q and iw[1] F, with Shoup companions
+  const void *fw, *iw;     // forward / inverse twiddle pairs {w, floor(w R / q)}, n entries
+};
+
+// c = a * b for `batch` polynomials of n = 2^logn words of io_bits (32/64) each, on stream s.
+// scr: three device buffers of batch * n words of word_bits, used only when n > 4096.
+hipError_t launch_polymul(const LaunchTables &T, const void *a, const void *b, void *c,
+                          size_t batch, int io_bits, void **scr, hipStream_t s);
+hipError_t launch_fill(void *a, void *b, uint32_t logn, uint64_t q, uint64_t seed, uint64_t p0,
+                       size_t count, int io_bits, hipStream_t s);
+hipError_t launch_check_range(const void *a, const void *b, uint64_t q, size_t total, int io_bits,
+                              int *bad, hipStream_t s);
+
+}  // namespace nttmul

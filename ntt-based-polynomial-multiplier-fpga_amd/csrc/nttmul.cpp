@@ -1,0 +1,346 @@
+// nttmul.cpp — host runtime behind include/nttmul.h (C ABI over the HIP runtime).
+//
+// Replaces the reference's host<->FPGA communicator one-for-one:
+//   PCIE_Load/PCIE_Open (PCIE.c:59-103, NTT_PCIECommunicationv2.c:274)  -> nttmul_create
+//   mode-0 DmaFifoWrite of W/W_INV/q/n_inv (NTT_PCIECommunicationv2.c:137-178)
+//                                                                      -> table upload in create
+//   mode-1/2 DmaFifoWrite(A/B) (:183-206)                              -> hipMemcpyAsync H2D
+//   mode-3 SendCommand + WaitForDoneAll polling (:211-215, :83-107)   -> launch + stream sync
+//   DmaFifoRead(C) (:220-224)                                          -> hipMemcpyAsync D2H
+//   szError + goto cleanup / return FALSE (:175-178, :242-251)         -> negative status codes
+// and provides the software path's entry points (ntt256_product1/4, NTT/ntt256.h:270-271) as
+// compat shims.  There is no CPU fallback anywhere in this library.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
+#include <vector>
+
+#include "launch.hpp"
+#include "nttmul.h"
+#include "planner.hpp"
+
+using namespace nttmul;
+
+namespace {
+
+constexpr int kMaxDev = 16;
+
+struct DevState {
+  int id = -1;
+  hipStream_t stream = nullptr;
+  void *fw = nullptr, *iw = nullptr;
+  void *scr[3] = {nullptr, nullptr, nullptr};
+  size_t scr_bytes = 0;
+  void *io[3] = {nullptr, nullptr, nullptr};  // host-path staging for a, b, c
+  size_t io_bytes = 0;
+  int *flag = nullptr;                        // range-check result
+};
+
+}  // namespace
+
+struct nttmul_ctx {
+  Plan plan;
+  uint32_t flags = 0;
+  int ndev = 0;
+  DevState dev[kMaxDev];
+  char err[256] = {0};
+};
+
+namespace {
+
+// Restores the caller's current device on scope exit (torch and others rely on it).
+struct DeviceGuard {
+  int prev = -1;
+  DeviceGuard() { (void)hipGetDevice(&prev); }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+int fail(nttmul_ctx *ctx, hipError_t e, const char *what) {
+  if (ctx) snprintf(ctx->err, sizeof(ctx->err), "%s: %s", what, hipGetErrorString(e));
+  return e == hipErrorOutOfMemory ? NTTMUL_ENOMEM : NTTMUL_EHIP;
+}
+
+#define HIP_TRY(ctx, expr)                          \
+  do {                                              \
+    hipError_t _e = (expr);                         \
+    if (_e != hipSuccess) return fail(ctx, _e, #expr); \
+  } while (0)
+
+LaunchTables tables_for(const nttmul_ctx *ctx, const DevState &d) {
+  const Plan &P = ctx->plan;
+  LaunchTables T;
+  T.logn = P.logn;
+  T.word_bits = P.word_bits;
+  T.q = P.q;
+  T.qinv_neg = P.qinv_neg;
+  T.f = P.f; T.fs = P.fs; T.wf = P.wf; T.wfs = P.wfs;
+  T.fw = d.fw;
+  T.iw = d.iw;
+  return T;
+}
+
+DevState *find_dev(nttmul_ctx *ctx, int dev) {
+  for (int i = 0; i < ctx->ndev; i++)
+    if (ctx->dev[i].id == dev) return &ctx->dev[i];
+  return nullptr;
+}
+
+int ensure(nttmul_ctx *ctx, void **bufs, int nb, size_t *have, size_t need) {
+  if (*have >= need) return NTTMUL_OK;
+  for (int i = 0; i < nb; i++) {
+    if (bufs[i]) (void)hipFree(bufs[i]);
+    bufs[i] = nullptr;
+  }
+  *have = 0;
+  for (int i = 0; i < nb; i++) HIP_TRY(ctx, hipMalloc(&bufs[i], need));
+  *have = need;
+  return NTTMUL_OK;
+}
+
+// Enqueue one device-resident batch on d (current device must be d.id).
+int run_device(nttmul_ctx *ctx, DevState &d, void *c, const void *a, const void *b, size_t batch,
+               int io_bits, hipStream_t s) {
+  const Plan &P = ctx->plan;
+  if (!batch) return NTTMUL_OK;
+  if (io_bits != 32 && io_bits != 64) return NTTMUL_EINVAL;
+  if (io_bits == 32 && P.q > 0xFFFFFFFFull) return NTTMUL_EINVAL;  // q does not fit the words
+  if (ctx->flags & NTTMUL_FLAG_VALIDATE) {
+    HIP_TRY(ctx, hipMemsetAsync(d.flag, 0, sizeof(int), s));
+    HIP_TRY(ctx, launch_check_range(a, b, P.q, batch * P.n, io_bits, d.flag, s));
+    int bad = 0;
+    HIP_TRY(ctx, hipMemcpyAsync(&bad, d.flag, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(ctx, hipStreamSynchronize(s));
+    if (bad) {
+      snprintf(ctx->err, sizeof(ctx->err), "input coefficient >= q");
+      return NTTMUL_ERANGE;
+    }
+  }
+  if (P.logn > 12) {
+    const size_t need = batch * (size_t)P.n * (P.word_bits / 8);
+    int st = ensure(ctx, d.scr, 3, &d.scr_bytes, need);
+    if (st) return st;
+  }
+  const LaunchTables T = tables_for(ctx, d);
+  HIP_TRY(ctx, launch_polymul(T, a, b, c, batch, io_bits, d.scr, s));
+  return NTTMUL_OK;
+}
+
+int multiply_host(nttmul_ctx *ctx, void *c, const void *a, const void *b, size_t batch,
+                  int io_bits) {
+  if (!ctx || !c || !a || !b) return NTTMUL_EINVAL;
+  if (!batch) return NTTMUL_OK;
+  DeviceGuard guard;
+  const size_t wb = io_bits / 8, n = ctx->plan.n;
+  // contiguous slices, one per device (no inter-device exchange)
+  size_t p0 = 0;
+  for (int i = 0; i < ctx->ndev; i++) {
+    const size_t p1 = batch * (size_t)(i + 1) / ctx->ndev;
+    const size_t cnt = p1 - p0;
+    DevState &d = ctx->dev[i];
+    if (cnt) {
+      HIP_TRY(ctx, hipSetDevice(d.id));
+      int st = ensure(ctx, d.io, 3, &d.io_bytes, cnt * n * wb);
+      if (st) return st;
+      const size_t off = p0 * n * wb, bytes = cnt * n * wb;
+      HIP_TRY(ctx, hipMemcpyAsync(d.io[0], (const char *)a + off, bytes, hipMemcpyHostToDevice,
+                                  d.stream));
+      HIP_TRY(ctx, hipMemcpyAsync(d.io[1], (const char *)b + off, bytes, hipMemcpyHostToDevice,
+                                  d.stream));
+      st = run_device(ctx, d, d.io[2], d.io[0], d.io[1], cnt, io_bits, d.stream);
+      if (st) return st;
+      HIP_TRY(ctx, hipMemcpyAsync((char *)c + off, d.io[2], bytes, hipMemcpyDeviceToHost,
+                                  d.stream));
+    }
+    p0 = p1;
+  }
+  for (int i = 0; i < ctx->ndev; i++) {
+    HIP_TRY(ctx, hipSetDevice(ctx->dev[i].id));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->dev[i].stream));
+  }
+  return NTTMUL_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *nttmul_strerror(int status) {
+  switch (status) {
+    case NTTMUL_OK: return "ok";
+    case NTTMUL_EINVAL: return "invalid argument (n, q, psi, word size or pointer)";
+    case NTTMUL_ENODEV: return "no usable HIP device";
+    case NTTMUL_EHIP: return "HIP runtime error";
+    case NTTMUL_ENOMEM: return "out of memory";
+    case NTTMUL_ERANGE: return "input coefficient out of range [0, q)";
+    case NTTMUL_EUNSUPPORTED: return "unsupported parameter combination";
+    default: return "unknown status";
+  }
+}
+
+const char *nttmul_last_error(const nttmul_ctx *ctx) { return ctx ? ctx->err : ""; }
+
+int nttmul_create_ex(nttmul_ctx **out, const nttmul_params *prm) {
+  if (!out || !prm) return NTTMUL_EINVAL;
+  *out = nullptr;
+  nttmul_ctx *ctx = new (std::nothrow) nttmul_ctx();
+  if (!ctx) return NTTMUL_ENOMEM;
+  int st = make_plan(prm->n, prm->q, prm->psi, &ctx->plan);
+  if (st) {
+    delete ctx;
+    return st;
+  }
+  ctx->flags = prm->flags;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+    delete ctx;
+    return NTTMUL_ENODEV;
+  }
+  const int first = prm->first_dev < 0 ? 0 : prm->first_dev;
+  int ndev = prm->ndev <= 0 ? count - first : prm->ndev;
+  if (first >= count || ndev <= 0 || first + ndev > count || ndev > kMaxDev) {
+    delete ctx;
+    return NTTMUL_ENODEV;
+  }
+  DeviceGuard guard;
+  const size_t tbytes = ctx->plan.fw.size();
+  for (int i = 0; i < ndev; i++) {
+    DevState &d = ctx->dev[i];
+    d.id = first + i;
+    ctx->ndev = i + 1;
+    hipError_t e;
+    if ((e = hipSetDevice(d.id)) != hipSuccess ||
+        (e = hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipMalloc(&d.fw, tbytes)) != hipSuccess || (e = hipMalloc(&d.iw, tbytes)) != hipSuccess ||
+        (e = hipMalloc((void **)&d.flag, sizeof(int))) != hipSuccess ||
+        (e = hipMemcpy(d.fw, ctx->plan.fw.data(), tbytes, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(d.iw, ctx->plan.iw.data(), tbytes, hipMemcpyHostToDevice)) != hipSuccess) {
+      st = fail(ctx, e, "nttmul_create device setup");
+      fprintf(stderr, "nttmul: %s\n", ctx->err);
+      nttmul_destroy(ctx);
+      return st == NTTMUL_EHIP ? NTTMUL_ENODEV : st;
+    }
+  }
+  *out = ctx;
+  return NTTMUL_OK;
+}
+
+int nttmul_create(nttmul_ctx **ctx, uint32_t n, uint64_t q, int ndev) {
+  nttmul_params p;
+  memset(&p, 0, sizeof(p));
+  p.n = n;
+  p.q = q;
+  p.ndev = ndev;
+  return nttmul_create_ex(ctx, &p);
+}
+
+void nttmul_destroy(nttmul_ctx *ctx) {
+  if (!ctx) return;
+  DeviceGuard guard;
+  for (int i = 0; i < ctx->ndev; i++) {
+    DevState &d = ctx->dev[i];
+    if (d.id < 0) continue;
+    (void)hipSetDevice(d.id);
+    if (d.stream) (void)hipStreamSynchronize(d.stream);
+    for (void *p : {d.fw, d.iw, (void *)d.flag, d.scr[0], d.scr[1], d.scr[2], d.io[0], d.io[1],
+                    d.io[2]})
+      if (p) (void)hipFree(p);
+    if (d.stream) (void)hipStreamDestroy(d.stream);
+  }
+  delete ctx;
+}
+
+int nttmul_get_info(const nttmul_ctx *ctx, nttmul_info *info) {
+  if (!ctx || !info) return NTTMUL_EINVAL;
+  const Plan &P = ctx->plan;
+  info->n = P.n;
+  info->logn = P.logn;
+  info->q = P.q;
+  info->psi = P.psi;
+  info->omega = P.omega;
+  info->inv_psi = P.inv_psi;
+  info->inv_omega = P.inv_omega;
+  info->inv_n = P.inv_n;
+  info->word_bits = (uint32_t)P.word_bits;
+  info->ndev = ctx->ndev;
+  info->kernel = P.logn > 12 ? 2 : 1;
+  return NTTMUL_OK;
+}
+
+int nttmul_multiply_batch_u32(nttmul_ctx *ctx, uint32_t *c, const uint32_t *a, const uint32_t *b,
+                              size_t batch) {
+  return multiply_host(ctx, c, a, b, batch, 32);
+}
+int nttmul_multiply_batch_u64(nttmul_ctx *ctx, uint64_t *c, const uint64_t *a, const uint64_t *b,
+                              size_t batch) {
+  return multiply_host(ctx, c, a, b, batch, 64);
+}
+int nttmul_multiply_u32(nttmul_ctx *ctx, uint32_t *c, const uint32_t *a, const uint32_t *b) {
+  return multiply_host(ctx, c, a, b, 1, 32);
+}
+int nttmul_multiply_u64(nttmul_ctx *ctx, uint64_t *c, const uint64_t *a, const uint64_t *b) {
+  return multiply_host(ctx, c, a, b, 1, 64);
+}
+
+int nttmul_multiply_batch_device(nttmul_ctx *ctx, void *c, const void *a, const void *b,
+                                 size_t batch, int word_bits, int dev, void *stream) {
+  if (!ctx || (batch && (!c || !a || !b))) return NTTMUL_EINVAL;
+  DevState *d = find_dev(ctx, dev);
+  if (!d) return NTTMUL_ENODEV;
+  DeviceGuard guard;
+  HIP_TRY(ctx, hipSetDevice(d->id));
+  return run_device(ctx, *d, c, a, b, batch, word_bits, (hipStream_t)stream);
+}
+
+int nttmul_fill_random_device(nttmul_ctx *ctx, void *a, void *b, uint64_t p0, size_t count,
+                              uint64_t seed, int word_bits, int dev, void *stream) {
+  if (!ctx || (count && (!a || !b)) || (word_bits != 32 && word_bits != 64)) return NTTMUL_EINVAL;
+  if (word_bits == 32 && ctx->plan.q > 0xFFFFFFFFull) return NTTMUL_EINVAL;
+  DevState *d = find_dev(ctx, dev);
+  if (!d) return NTTMUL_ENODEV;
+  DeviceGuard guard;
+  HIP_TRY(ctx, hipSetDevice(d->id));
+  HIP_TRY(ctx, launch_fill(a, b, ctx->plan.logn, ctx->plan.q, seed, p0, count, word_bits,
+                           (hipStream_t)stream));
+  return NTTMUL_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Compat shims: the reference's software-path entry points (n = 256, q = 12289, psi = 1002).
+// ---------------------------------------------------------------------------------------------
+static nttmul_ctx *g_ctx256 = nullptr;
+static std::once_flag g_once256;
+static std::mutex g_mu256;
+
+static void product256(int32_t *c, const int32_t *a, const int32_t *b) {
+  std::call_once(g_once256, [] {
+    nttmul_params p;
+    memset(&p, 0, sizeof(p));
+    p.n = 256;
+    p.q = 12289;
+    p.psi = 1002;  // ntt256_tables.h:20
+    p.ndev = 1;
+    int st = nttmul_create_ex(&g_ctx256, &p);
+    if (st) {
+      fprintf(stderr, "nttmul: ntt256 context: %s\n", nttmul_strerror(st));
+      abort();
+    }
+  });
+  std::lock_guard<std::mutex> lock(g_mu256);
+  int st = nttmul_multiply_u32(g_ctx256, (uint32_t *)c, (const uint32_t *)a, (const uint32_t *)b);
+  if (st) {
+    fprintf(stderr, "nttmul: ntt256 product: %s (%s)\n", nttmul_strerror(st), g_ctx256->err);
+    abort();
+  }
+}
+
+void ntt256_product1(int32_t *c, int32_t *a, int32_t *b) { product256(c, a, b); }
+void ntt256_product4(int32_t *c, int32_t *a, int32_t *b) { product256(c, a, b); }
+void ntt_red256_product1(int32_t *c, int32_t *a, int32_t *b) { product256(c, a, b); }
+void ntt_red256_product4(int32_t *c, int32_t *a, int32_t *b) { product256(c, a, b); }
+
+}  // extern "C"

@@ -1,0 +1,142 @@
+// planner.cpp — see planner.hpp.
+#include "planner.hpp"
+
+#include <string.h>
+
+#include "nttmul.h"
+
+namespace nttmul {
+
+typedef unsigned __int128 u128;
+
+uint64_t mulmod(uint64_t a, uint64_t b, uint64_t q) { return (uint64_t)(((u128)a * b) % q); }
+
+uint64_t powmod(uint64_t b, uint64_t e, uint64_t q) {
+  uint64_t r = 1 % q;
+  b %= q;
+  for (; e; e >>= 1) {
+    if (e & 1) r = mulmod(r, b, q);
+    b = mulmod(b, b, q);
+  }
+  return r;
+}
+
+// prime_generate.C:23 miller_rabin, made deterministic for 64-bit inputs (fixed witness set).
+bool is_prime(uint64_t n) {
+  static const uint64_t wit[] = {2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37};
+  if (n < 2) return false;
+  for (uint64_t p : wit) {
+    if (n == p) return true;
+    if (n % p == 0) return false;
+  }
+  uint64_t d = n - 1;
+  int s = 0;
+  while (!(d & 1)) { d >>= 1; s++; }
+  for (uint64_t a : wit) {
+    uint64_t x = powmod(a, d, n);
+    if (x == 1 || x == n - 1) continue;
+    bool composite = true;
+    for (int r = 1; r < s && composite; r++) {
+      x = mulmod(x, x, n);
+      if (x == n - 1) composite = false;
+    }
+    if (composite) return false;
+  }
+  return true;
+}
+
+uint64_t smallest_psi(uint32_t n, uint64_t q) {
+  const uint64_t two_n = 2ull * n;
+  if ((q - 1) % two_n) return 0;
+  uint64_t r = 0;
+  for (uint64_t g = 2; g < q && !r; g++) {
+    uint64_t c = powmod(g, (q - 1) / two_n, q);
+    if (powmod(c, n, q) == q - 1) r = c;  // order exactly 2n
+  }
+  if (!r) return 0;
+  // the primitive 2n-th roots are r^k, k odd: take the least
+  uint64_t r2 = mulmod(r, r, q), cur = r, best = r;
+  for (uint64_t k = 3; k < two_n; k += 2) {
+    cur = mulmod(cur, r2, q);
+    if (cur < best) best = cur;
+  }
+  return best;
+}
+
+static uint32_t bitrev(uint32_t x, uint32_t bits) {
+  uint32_t r = 0;
+  for (uint32_t i = 0; i < bits; i++) r |= ((x >> i) & 1u) << (bits - 1 - i);
+  return r;
+}
+
+static uint64_t companion(uint64_t w, uint64_t q, int bits) {
+  return (uint64_t)(((u128)w << bits) / q);
+}
+
+template <class W>
+static void put_pairs(std::vector<uint8_t> &dst, const std::vector<uint64_t> &w, uint64_t q,
+                      int bits) {
+  dst.assign(w.size() * 2 * sizeof(W), 0);
+  W *p = (W *)dst.data();
+  for (size_t i = 0; i < w.size(); i++) {
+    p[2 * i] = (W)w[i];
+    p[2 * i + 1] = (W)companion(w[i], q, bits);
+  }
+}
+
+int make_plan(uint32_t n, uint64_t q, uint64_t psi, Plan *P) {
+  if (n < 256 || n > 65536 || (n & (n - 1))) return NTTMUL_EINVAL;
+  if (q < 3 || q >= (1ull << 62) || !is_prime(q) || (q - 1) % (2ull * n)) return NTTMUL_EINVAL;
+  if (!psi) psi = smallest_psi(n, q);
+  if (!psi || psi >= q || powmod(psi, n, q) != q - 1) return NTTMUL_EINVAL;
+  P->n = n;
+  P->logn = 0;
+  while ((1u << P->logn) < n) P->logn++;
+  P->q = q;
+  P->psi = psi;
+  P->omega = mulmod(psi, psi, q);
+  P->inv_psi = powmod(psi, q - 2, q);
+  P->inv_omega = mulmod(P->inv_psi, P->inv_psi, q);
+  P->inv_n = powmod(n, q - 2, q);
+  P->word_bits = q < (1ull << 31) ? 32 : 64;
+  const int bits = P->word_bits;
+
+  // psi^k, k in [0, 2n): every twiddle is a power of psi (psi^(2n) = 1)
+  const uint32_t two_n = 2 * n;
+  std::vector<uint64_t> pw(two_n);
+  pw[0] = 1;
+  for (uint32_t k = 1; k < two_n; k++) pw[k] = mulmod(pw[k - 1], psi, q);
+  // mixed_powers_rev[t+j] = psi^(n/2t) omega^((n/2t) bitrev(j)) = psi^(e (1 + 2 bitrev(j))),
+  // inv_mixed_powers_rev = its inverse (ntt.h:120-127, :145-155; ntt256.h:58,63)
+  std::vector<uint64_t> fw(n, 0), iw(n, 0);
+  uint32_t lt = 0;
+  for (uint32_t t = 1; t < n; t <<= 1, lt++) {
+    const uint64_t e = n / (2ull * t);
+    for (uint32_t j = 0; j < t; j++) {
+      const uint64_t ex = (e * (1 + 2ull * bitrev(j, lt))) % two_n;
+      fw[t + j] = pw[ex];
+      iw[t + j] = pw[(two_n - ex) % two_n];
+    }
+  }
+  if (bits == 32) {
+    put_pairs<uint32_t>(P->fw, fw, q, 32);
+    put_pairs<uint32_t>(P->iw, iw, q, 32);
+  } else {
+    put_pairs<uint64_t>(P->fw, fw, q, 64);
+    put_pairs<uint64_t>(P->iw, iw, q, 64);
+  }
+  // Montgomery constant -q^-1 mod 2^bits (Newton on 2-adic inverse)
+  uint64_t inv = q;
+  for (int i = 0; i < 6; i++) inv *= 2 - q * inv;
+  P->qinv_neg = (0 - inv) & (bits == 32 ? 0xFFFFFFFFull : ~0ull);
+  // F = n^-1 R mod q, R = 2^bits: cancels the Montgomery R^-1 of the pointwise product and the
+  // n of the unnormalised inverse transform (ntt256.C:12 scaled_inv_psi_powers' n^-1).
+  const uint64_t r_mod_q = (uint64_t)(((u128)1 << bits) % q);
+  P->f = mulmod(P->inv_n, r_mod_q, q);
+  P->fs = companion(P->f, q, bits);
+  P->wf = mulmod(iw[1], P->f, q);
+  P->wfs = companion(P->wf, q, bits);
+  return NTTMUL_OK;
+}
+
+}  // namespace nttmul

@@ -1,0 +1,211 @@
+"""Python host mirror of the nttmul C ABI (include/nttmul.h), over ctypes.
+
+This is the reference-side binding a Python caller uses: it exposes the reference's product entry
+points with their names and argument meaning (ntt256_product1/4, ntt_red256_product1/4:
+NTT/ntt256.h:270-271, NTT-RED/ntt_red256.h:87,90 — output array c, inputs a, b, n = 256,
+q = 12289) plus the generic batched API multiply(a, b) for any (n, q).  All compute runs in
+lib/libnttmul.so on the GPU; there is no CPU fallback: if the library or a GPU is missing the calls
+raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libnttmul.so")
+HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "nttmul.h")
+
+NTTMUL_OK = 0
+NTTMUL_EINVAL = -1
+NTTMUL_ENODEV = -2
+NTTMUL_EHIP = -3
+NTTMUL_ENOMEM = -4
+NTTMUL_ERANGE = -5
+NTTMUL_EUNSUPPORTED = -6
+NTTMUL_FLAG_VALIDATE = 1
+
+SEED = 0x4E54544D554C  # "NTTMUL", SURVEY §8d
+
+
+class NttmulError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"nttmul status {status}: {msg}")
+        self.status = status
+
+
+class _Params(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint32), ("q", ctypes.c_uint64), ("psi", ctypes.c_uint64),
+                ("ndev", ctypes.c_int), ("first_dev", ctypes.c_int), ("flags", ctypes.c_uint32)]
+
+
+class Info(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint32), ("logn", ctypes.c_uint32), ("q", ctypes.c_uint64),
+                ("psi", ctypes.c_uint64), ("omega", ctypes.c_uint64),
+                ("inv_psi", ctypes.c_uint64), ("inv_omega", ctypes.c_uint64),
+                ("inv_n", ctypes.c_uint64), ("word_bits", ctypes.c_uint32),
+                ("ndev", ctypes.c_int), ("kernel", ctypes.c_int)]
+
+
+_LIB: Optional[ctypes.CDLL] = None
+
+
+def load_library() -> ctypes.CDLL:
+    """Load lib/libnttmul.so (built by `make -C ntt-based-polynomial-multiplier-fpga_amd`)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not built: run __graft_entry__.build() or make -C {PKG_DIR}")
+    lib = ctypes.CDLL(LIB_PATH)
+    vp, sz, u64, u32, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+    lib.nttmul_create.argtypes = [ctypes.POINTER(vp), u32, u64, i32]
+    lib.nttmul_create_ex.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(_Params)]
+    lib.nttmul_destroy.argtypes = [vp]
+    lib.nttmul_destroy.restype = None
+    lib.nttmul_strerror.argtypes = [i32]
+    lib.nttmul_strerror.restype = ctypes.c_char_p
+    lib.nttmul_last_error.argtypes = [vp]
+    lib.nttmul_last_error.restype = ctypes.c_char_p
+    lib.nttmul_get_info.argtypes = [vp, ctypes.POINTER(Info)]
+    for name in ("nttmul_multiply_u32", "nttmul_multiply_u64"):
+        getattr(lib, name).argtypes = [vp, vp, vp, vp]
+    for name in ("nttmul_multiply_batch_u32", "nttmul_multiply_batch_u64"):
+        getattr(lib, name).argtypes = [vp, vp, vp, vp, sz]
+    lib.nttmul_multiply_batch_device.argtypes = [vp, vp, vp, vp, sz, i32, i32, vp]
+    lib.nttmul_fill_random_device.argtypes = [vp, vp, vp, u64, sz, u64, i32, i32, vp]
+    for name in ("ntt256_product1", "ntt256_product4", "ntt_red256_product1", "ntt_red256_product4"):
+        getattr(lib, name).argtypes = [vp, vp, vp]
+        getattr(lib, name).restype = None
+    _LIB = lib
+    return lib
+
+
+def exported_symbols() -> list:
+    """Function names declared in include/nttmul.h (for the ABI completeness test)."""
+    import re
+    text = open(HEADER_PATH).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?(?:int|void|char\s*\*|const char \*)\s*\*?\s*"
+                                 r"(nttmul_\w+|ntt256_\w+|ntt_red256_\w+)\s*\(", text, re.M)))
+
+
+def strerror(status: int) -> str:
+    return load_library().nttmul_strerror(status).decode()
+
+
+def _ptr(x) -> int:
+    """Raw address of a numpy array or a torch tensor (device pointer for CUDA/HIP tensors)."""
+    if isinstance(x, np.ndarray):
+        assert x.flags.c_contiguous
+        return x.ctypes.data
+    if hasattr(x, "data_ptr"):
+        assert x.is_contiguous()
+        return x.data_ptr()
+    return int(x)
+
+
+class Context:
+    """An (n, q) multiplier bound to one or more HIP devices (≙ an opened FPGA handle)."""
+
+    def __init__(self, n: int, q: int, psi: int = 0, ndev: int = 1, first_dev: int = 0,
+                 validate: bool = False):
+        self._lib = load_library()
+        self._h = ctypes.c_void_p()
+        prm = _Params(n, q, psi, ndev, first_dev, NTTMUL_FLAG_VALIDATE if validate else 0)
+        st = self._lib.nttmul_create_ex(ctypes.byref(self._h), ctypes.byref(prm))
+        if st != NTTMUL_OK:
+            raise NttmulError(st, strerror(st))
+        info = Info()
+        self._lib.nttmul_get_info(self._h, ctypes.byref(info))
+        self.info = info
+        self.n, self.q, self.psi = info.n, info.q, info.psi
+        self.word_bits = info.word_bits
+        self.first_dev = first_dev
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            self._lib.nttmul_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, st: int):
+        if st != NTTMUL_OK:
+            raise NttmulError(st, f"{strerror(st)}: {self._lib.nttmul_last_error(self._h).decode()}")
+
+    @property
+    def io_dtype(self):
+        return np.uint32 if self.q < (1 << 32) else np.uint64
+
+    def multiply(self, a, b, dtype=None) -> np.ndarray:
+        """c = a * b mod (x^n + 1, q) for host arrays of shape [n] or [batch, n]."""
+        dtype = dtype or self.io_dtype
+        a = np.ascontiguousarray(a, dtype=dtype)
+        b = np.ascontiguousarray(b, dtype=dtype)
+        if a.shape != b.shape or a.shape[-1] != self.n:
+            raise ValueError("a and b must both have shape [..., n]")
+        c = np.empty_like(a)
+        batch = a.size // self.n
+        fn = self._lib.nttmul_multiply_batch_u32 if dtype == np.uint32 else self._lib.nttmul_multiply_batch_u64
+        self._check(fn(self._h, c.ctypes.data, a.ctypes.data, b.ctypes.data, batch))
+        return c
+
+    def multiply_device(self, c, a, b, batch: int, word_bits: int, dev: Optional[int] = None,
+                        stream: int = 0):
+        """Device-resident batch (pointers or torch tensors on `dev`), enqueued on `stream`."""
+        dev = self.first_dev if dev is None else dev
+        self._check(self._lib.nttmul_multiply_batch_device(self._h, _ptr(c), _ptr(a), _ptr(b), batch,
+                                                           word_bits, dev, stream or None))
+
+    def fill_random_device(self, a, b, p0: int, count: int, word_bits: int, seed: int = SEED,
+                           dev: Optional[int] = None, stream: int = 0):
+        dev = self.first_dev if dev is None else dev
+        self._check(self._lib.nttmul_fill_random_device(self._h, _ptr(a), _ptr(b), p0, count, seed,
+                                                        word_bits, dev, stream or None))
+
+
+def multiply(a, b, n: int, q: int) -> np.ndarray:
+    """multiply(a, b, n, q) -> c: the north-star entry point, one-shot."""
+    with Context(n, q) as ctx:
+        return ctx.multiply(a, b)
+
+
+def _product256(name: str, c: np.ndarray, a: np.ndarray, b: np.ndarray) -> None:
+    for x in (a, b, c):
+        if not (isinstance(x, np.ndarray) and x.dtype == np.int32 and x.size == 256
+                and x.flags.c_contiguous):
+            raise TypeError("ntt256 products take contiguous int32 arrays of 256 coefficients")
+    getattr(load_library(), name)(c.ctypes.data, a.ctypes.data, b.ctypes.data)
+
+
+def ntt256_product1(c: np.ndarray, a: np.ndarray, b: np.ndarray) -> None:
+    """NTT/ntt256.C:5 — c = a * b at n = 256, q = 12289 (result written into c)."""
+    _product256("ntt256_product1", c, a, b)
+
+
+def ntt256_product4(c: np.ndarray, a: np.ndarray, b: np.ndarray) -> None:
+    """NTT/ntt256.C:16."""
+    _product256("ntt256_product4", c, a, b)
+
+
+def ntt_red256_product1(c: np.ndarray, a: np.ndarray, b: np.ndarray) -> None:
+    """NTT-RED/ntt_red256.C:5."""
+    _product256("ntt_red256_product1", c, a, b)
+
+
+def ntt_red256_product4(c: np.ndarray, a: np.ndarray, b: np.ndarray) -> None:
+    """NTT-RED/ntt_red256.C:30."""
+    _product256("ntt_red256_product4", c, a, b)

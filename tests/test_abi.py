@@ -1,0 +1,52 @@
+"""CPU tests of the C ABI boundary: the library loads, exports every entry point include/nttmul.h
+declares, and reports errors (never falls back to a CPU path) when no GPU is present."""
+import ctypes
+import os
+import subprocess
+
+import pytest
+
+import nttmul
+
+
+def test_library_exports_every_declared_symbol():
+    lib = nttmul.load_library()
+    syms = nttmul.exported_symbols()
+    expected = {"nttmul_create", "nttmul_create_ex", "nttmul_destroy", "nttmul_strerror",
+                "nttmul_last_error", "nttmul_get_info", "nttmul_multiply_u32",
+                "nttmul_multiply_u64", "nttmul_multiply_batch_u32", "nttmul_multiply_batch_u64",
+                "nttmul_multiply_batch_device", "nttmul_fill_random_device", "ntt256_product1",
+                "ntt256_product4", "ntt_red256_product1", "ntt_red256_product4"}
+    assert expected <= set(syms), set(expected) - set(syms)
+    for s in syms:
+        assert hasattr(lib, s), s
+
+
+def test_exports_are_plain_c_abi():
+    out = subprocess.run(["nm", "-D", "--defined-only", nttmul.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    names = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    for s in nttmul.exported_symbols():
+        assert s in names, f"{s} missing or C++-mangled"
+
+
+def test_strerror_and_invalid_params():
+    assert nttmul.strerror(0) == "ok"
+    assert "range" in nttmul.strerror(nttmul.NTTMUL_ERANGE)
+    lib = nttmul.load_library()
+    h = ctypes.c_void_p()
+    # parameter validation happens before any device access
+    assert lib.nttmul_create(ctypes.byref(h), 1000, 2013265921, 1) == nttmul.NTTMUL_EINVAL
+    assert lib.nttmul_create(ctypes.byref(h), 4096, 12289, 1) == nttmul.NTTMUL_EINVAL  # no 8192th root
+    assert lib.nttmul_create(ctypes.byref(h), 4096, 2013265923, 1) == nttmul.NTTMUL_EINVAL  # composite
+    assert lib.nttmul_create(ctypes.byref(h), 4096, (1 << 62) + 1, 1) == nttmul.NTTMUL_EINVAL
+    assert lib.nttmul_create(ctypes.byref(h), 128, 12289, 1) == nttmul.NTTMUL_EINVAL  # n < 256
+
+
+@pytest.mark.skipif(os.environ.get("HIP_VISIBLE_DEVICES") is None and os.path.exists("/dev/kfd"),
+                    reason="a GPU may be present")
+def test_no_gpu_fails_loudly():
+    """Without a HIP device there is no silent CPU fallback: create returns NTTMUL_ENODEV."""
+    with pytest.raises(nttmul.NttmulError) as ei:
+        nttmul.Context(4096, 2013265921)
+    assert ei.value.status == nttmul.NTTMUL_ENODEV

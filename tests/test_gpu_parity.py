@@ -1,0 +1,215 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the oracle and the golden fixtures.
+
+Bit-exact integer results are required everywhere.  Sizes are those the oracle finishes in
+seconds; at BASELINE.json's full sizes the tests check sampled polymults (inputs are counter-based,
+so the oracle regenerates any one) and size-independent properties (linearity, ragged batches).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import nttmul
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+Q0 = 12289
+Q31 = 2013265921            # 15 * 2^27 + 1, the benchmark modulus
+Q30 = 1073479681            # < 2^30
+Q32 = 4293918721            # 0xFFF00001, full 32-bit word
+Q62 = 0x3FFFFFFFFFE80001    # 62-bit, 2^17 | q - 1
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def _ctx(n, q, psi=0, **kw):
+    return nttmul.Context(n, q, psi=psi, **kw)
+
+
+def test_native_library_is_loaded_and_on_gpu(torch_cuda):
+    ctx = _ctx(4096, Q31)
+    assert ctx.info.ndev >= 1 and ctx.word_bits == 32 and ctx.info.kernel == 1
+    assert os.path.samefile(nttmul.LIB_PATH, nttmul.load_library()._name)
+
+
+def _kats(golden_dir):
+    data = json.load(open(os.path.join(golden_dir, "kat256.json")))
+    for kat in data["kats"]:
+        vecs = []
+        for key in ("a", "b", "c"):
+            v = np.zeros(256, dtype=np.int32)
+            for i, x in kat[key].items():
+                v[int(i)] = x
+            vecs.append(v)
+        yield kat["name"], vecs
+
+
+def test_compat_shims_kats(golden_dir, torch_cuda):
+    """ntt256_product1/4 and ntt_red256_product1/4 with the reference's signatures."""
+    for name, (a, b, c) in _kats(golden_dir):
+        for fn in (nttmul.ntt256_product1, nttmul.ntt256_product4, nttmul.ntt_red256_product1,
+                   nttmul.ntt_red256_product4):
+            out = np.zeros(256, dtype=np.int32)
+            fn(out, a.copy(), b.copy())
+            assert np.array_equal(out, c), (name, fn.__name__)
+
+
+def test_ref256_golden(golden_dir, torch_cuda):
+    """The reference's own coefficient files + 63 vectors: all four reference products agree with
+    the GPU (batched, psi = 1002 as ntt256_tables.h:20)."""
+    g = np.load(os.path.join(golden_dir, "ref256.npz"))
+    ctx = _ctx(256, Q0, psi=1002)
+    c = ctx.multiply(g["a"], g["b"])
+    for name in ("ntt256_product1", "ntt256_product4", "ntt_red256_product1", "ntt_red256_product4"):
+        assert np.array_equal(c, g[name]), name
+    out = np.zeros(256, dtype=np.int32)
+    nttmul.ntt256_product4(out, g["a"][0].astype(np.int32), g["b"][0].astype(np.int32))
+    assert np.array_equal(out, g["ntt256_product4"][0].astype(np.int32))
+
+
+def test_ref_generic_golden(golden_dir, torch_cuda):
+    g = np.load(os.path.join(golden_dir, "ref_generic_12289.npz"))
+    for n in (512, 1024, 2048):
+        ctx = _ctx(n, Q0)
+        assert ctx.psi == int(g[f"n{n}_psi"][0])
+        assert np.array_equal(ctx.multiply(g[f"n{n}_a"], g[f"n{n}_b"]), g[f"n{n}_c"]), n
+
+
+def test_schoolbook_bigint_golden(golden_dir, torch_cuda):
+    g = np.load(os.path.join(golden_dir, "schoolbook_bigint.npz"))
+    keys = sorted({k.rsplit("_", 1)[0] for k in g.files})
+    for key in keys:
+        n = int(key.split("_")[0][1:])
+        q = int(key.split("_")[1][1:])
+        ctx = _ctx(n, q)
+        dt = np.uint32 if q < (1 << 32) else np.uint64
+        c = ctx.multiply(g[key + "_a"].astype(dt), g[key + "_b"].astype(dt))
+        assert np.array_equal(c.astype(np.uint64), g[key + "_c"]), key
+        if q < (1 << 32):  # u32 words through the 64-bit kernels as well
+            c64 = ctx.multiply(g[key + "_a"], g[key + "_b"], dtype=np.uint64)
+            assert np.array_equal(c64, g[key + "_c"]), key
+
+
+@pytest.mark.parametrize("n", [256, 512, 1024, 2048, 4096])
+@pytest.mark.parametrize("q", [Q31, Q30, Q32, Q62])
+def test_random_vs_oracle(n, q, torch_cuda):
+    """Ragged batch sizes (partial blocks) against the restated psi-merged product."""
+    P = O.Plan(n, q)
+    ctx = _ctx(n, q)
+    for batch in (1, 3, 17):
+        a, b = O.fill_inputs(n, q, 1000 + batch, batch)
+        if batch == 17:
+            a[0] = q - 1; b[0] = q - 1          # all (q-1)
+            a[1] = 0                            # zero polynomial
+            a[2] = 0; a[2, n - 1] = 1           # x^(n-1) * x^(n-1) = -x^(n-2)
+            b[2] = 0; b[2, n - 1] = 1
+        dt = np.uint32 if q < (1 << 32) else np.uint64
+        c = ctx.multiply(a.astype(dt), b.astype(dt)).astype(np.uint64)
+        for i in range(batch):
+            assert np.array_equal(c[i], P.product_merged(a[i], b[i])), (n, q, batch, i)
+        if batch == 17:
+            assert not c[1].any()
+            exp = np.zeros(n, dtype=np.uint64); exp[n - 2] = q - 1
+            assert np.array_equal(c[2], exp)
+
+
+@pytest.mark.parametrize("n", [8192, 16384, 32768, 65536])
+@pytest.mark.parametrize("q", [Q31, Q62])
+def test_multipass_vs_oracle(n, q, torch_cuda):
+    """n > 4096: column pass + fused rows + inverse column pass."""
+    P = O.Plan(n, q)
+    ctx = _ctx(n, q)
+    assert ctx.info.kernel == 2
+    a, b = O.fill_inputs(n, q, 7, 2)
+    a[1] = q - 1
+    dt = np.uint32 if q < (1 << 32) else np.uint64
+    c = ctx.multiply(a.astype(dt), b.astype(dt)).astype(np.uint64)
+    for i in range(2):
+        assert np.array_equal(c[i], P.product_merged(a[i], b[i])), (n, q, i)
+    assert P.eval_check(c[0], a[0], b[0], points=2) == 0
+
+
+def _torch_dtype(torch, word_bits):
+    return torch.int32 if word_bits == 32 else torch.int64
+
+
+def _as_np(t, word_bits):
+    arr = t.cpu().numpy()
+    return arr.view(np.uint32 if word_bits == 32 else np.uint64)
+
+
+@pytest.mark.parametrize("n,q,word_bits,batch", [(4096, Q31, 32, 65536), (1024, Q31, 32, 4096),
+                                                  (65536, Q62, 64, 1024)])
+def test_full_size_device_path(n, q, word_bits, batch, torch_cuda):
+    """BASELINE configs C2/C3/C5 at full size on device-resident data: sampled polymults against
+    the oracle (inputs regenerated from the counter) and linearity over the whole batch."""
+    torch = torch_cuda
+    ctx = _ctx(n, q)
+    dt = _torch_dtype(torch, word_bits)
+    a = torch.empty(batch * n, dtype=dt, device="cuda")
+    b = torch.empty_like(a)
+    c = torch.empty_like(a)
+    stream = torch.cuda.current_stream().cuda_stream
+    ctx.fill_random_device(a, b, 0, batch, word_bits, stream=stream)
+    ctx.multiply_device(c, a, b, batch, word_bits, stream=stream)
+    torch.cuda.synchronize()
+    P = O.Plan(n, q)
+    rng = np.random.default_rng(n + batch)
+    for p in sorted(set([0, batch - 1] + list(rng.integers(0, batch, 2)))):
+        ea, eb = O.fill_inputs(n, q, int(p), 1)
+        assert np.array_equal(_as_np(a[p * n:(p + 1) * n], word_bits).astype(np.uint64), ea[0])
+        got = _as_np(c[p * n:(p + 1) * n], word_bits).astype(np.uint64)
+        assert np.array_equal(got, P.product_merged(ea[0], eb[0])), p
+    # linearity over the whole batch: (a + a') * b == a*b + a'*b  (mod q), checked on the GPU
+    if word_bits == 32:
+        a2 = torch.empty_like(a)
+        d = torch.empty_like(a)
+        ctx.fill_random_device(a2, d, batch, batch, word_bits, stream=stream)  # fresh a'
+        s = ((a.long() & 0xFFFFFFFF) + (a2.long() & 0xFFFFFFFF)) % q
+        s32 = s.to(torch.int32)
+        c_s = torch.empty_like(a)
+        c_2 = torch.empty_like(a)
+        ctx.multiply_device(c_s, s32, b, batch, word_bits, stream=stream)
+        ctx.multiply_device(c_2, a2, b, batch, word_bits, stream=stream)
+        torch.cuda.synchronize()
+        lhs = c_s.long() & 0xFFFFFFFF
+        rhs = ((c.long() & 0xFFFFFFFF) + (c_2.long() & 0xFFFFFFFF)) % q
+        assert torch.equal(lhs, rhs)
+        assert int((c.long() & 0xFFFFFFFF).max()) < q
+
+
+def test_validate_flag(torch_cuda):
+    ctx = _ctx(1024, Q31, validate=True)
+    a, b = O.fill_inputs(1024, Q31, 0, 2)
+    a = a.astype(np.uint32); b = b.astype(np.uint32)
+    ctx.multiply(a, b)
+    a[1, 5] = Q31
+    with pytest.raises(nttmul.NttmulError) as ei:
+        ctx.multiply(a, b)
+    assert ei.value.status == nttmul.NTTMUL_ERANGE
+
+
+def test_single_multiply_entry(torch_cuda):
+    a, b = O.fill_inputs(4096, Q31, 3, 1)
+    c = nttmul.multiply(a[0], b[0], 4096, Q31)
+    assert np.array_equal(c.astype(np.uint64), O.Plan(4096, Q31).product_merged(a[0], b[0]))
+
+
+def test_multi_device_context_split(torch_cuda):
+    torch = torch_cuda
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs 2 GPUs")
+    ctx = _ctx(2048, Q31, ndev=2)
+    a, b = O.fill_inputs(2048, Q31, 0, 9)
+    c = ctx.multiply(a.astype(np.uint32), b.astype(np.uint32)).astype(np.uint64)
+    P = O.Plan(2048, Q31)
+    for i in range(9):
+        assert np.array_equal(c[i], P.product_merged(a[i], b[i]))
