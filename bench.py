@@ -34,6 +34,32 @@ def shard(global_batch: int, rank: int, world: int):
     return p0, p1
 
 
+def timed_steps(step, steps: int, warmup: int, sync, barrier):
+    """W untimed warmup steps, then K timed steps bracketed by barrier + device sync on both
+    sides (the driver's contract); returns the wall seconds of the K steps on this rank."""
+    for _ in range(warmup):
+        step()
+    sync()
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    barrier()
+    sync()
+    return time.perf_counter() - t0
+
+
+def max_over_ranks(x: float, dist, device) -> float:
+    """Max of a per-rank float over the process group (identity when not distributed)."""
+    import torch
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -122,31 +148,22 @@ def main(argv=None):
     def step():
         ctx.multiply_device(c, a, b, p1 - p0, wb, stream=sptr)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        step()
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    wall = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / args.steps   # HIP events on the launch stream
+    events = {"n": 0}
 
-    wall_t = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
-    wall_max = float(wall_t.item())
+    def timed_step():  # HIP events on the launch stream around the K timed steps
+        if events["n"] == args.warmup:
+            ev0.record(stream)
+        step()
+        events["n"] += 1
+        if events["n"] == args.warmup + args.steps:
+            ev1.record(stream)
+
+    wall = timed_steps(timed_step, args.steps, args.warmup, lambda: torch.cuda.synchronize(dev),
+                       (lambda: dist.barrier()) if world > 1 else (lambda: None))
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
+    wall_max = max_over_ranks(wall, dist if world > 1 else None, dev)
 
     if rank == 0:
         value = global_batch * args.steps / wall_max

@@ -24,6 +24,25 @@
 #include "launch.hpp"
 #include "modarith.hpp"
 
+// LDS regions per polynomial pair (2: a and b exchanged together; 1: in turn, half the LDS)
+#ifndef NTTMUL_LDS_REGIONS
+#define NTTMUL_LDS_REGIONS 2
+#endif
+// __launch_bounds__ minimum waves per SIMD for k_rows (1 = no constraint)
+#ifndef NTTMUL_MIN_WAVES
+#define NTTMUL_MIN_WAVES 1
+#endif
+// Ablation switches for tools/kbench timing builds only (results are wrong when set).
+#ifndef NTTMUL_ABL_NOLOAD
+#define NTTMUL_ABL_NOLOAD 0
+#endif
+#ifndef NTTMUL_ABL_NOXCHG
+#define NTTMUL_ABL_NOXCHG 0
+#endif
+#ifndef NTTMUL_ABL_NOSTORE
+#define NTTMUL_ABL_NOSTORE 0
+#endif
+
 namespace nttmul {
 
 template <class A>
@@ -138,14 +157,32 @@ __device__ __forceinline__ void inv_group(const KParams<A> &P, typename A::word 
 template <int LOGS, int gfrom, int gto, int NREG, class W>
 __device__ __forceinline__ void exchange(W (&x)[16], W (&y)[16], W *lds_x, W *lds_y, int j) {
   using Gr = Groups<LOGS>;
+#if NTTMUL_ABL_NOXCHG
+  return;
+#endif
   const int bw = Gr::pad(Gr::base(gfrom, j));
+  const int br = Gr::pad(Gr::base(gto, j));
+  if (NTTMUL_LDS_REGIONS == 1 && NREG == 2) {  // one region, the two polynomials in turn
+#pragma unroll
+    for (int k = 0; k < 16; k++) lds_x[bw + Gr::pad(Gr::off(gfrom, k))] = x[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; k++) x[k] = lds_x[br + Gr::pad(Gr::off(gto, k))];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; k++) lds_x[bw + Gr::pad(Gr::off(gfrom, k))] = y[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; k++) y[k] = lds_x[br + Gr::pad(Gr::off(gto, k))];
+    __syncthreads();
+    return;
+  }
 #pragma unroll
   for (int k = 0; k < 16; k++) {
     lds_x[bw + Gr::pad(Gr::off(gfrom, k))] = x[k];
     if (NREG == 2) lds_y[bw + Gr::pad(Gr::off(gfrom, k))] = y[k];
   }
   __syncthreads();
-  const int br = Gr::pad(Gr::base(gto, j));
 #pragma unroll
   for (int k = 0; k < 16; k++) {
     x[k] = lds_x[br + Gr::pad(Gr::off(gto, k))];
@@ -186,31 +223,49 @@ __device__ __forceinline__ void inv_all(const KParams<A> &P, typename A::word (&
 //   L1 >  0 : unit u is row (u mod 2^L1) of polynomial (u >> L1) after the column pass; the
 //             row's stages are global stages L1 .. L1+LOGS-1; output stays lazy in [0, 2q).
 template <class A, class TIn, class TOut, int LOGS, int L1>
-__global__ __launch_bounds__(256) void k_rows(KParams<A> P, const TIn *__restrict__ a,
+__global__ __launch_bounds__(256, NTTMUL_MIN_WAVES) void k_rows(KParams<A> P, const TIn *__restrict__ a,
                                               const TIn *__restrict__ b, TOut *__restrict__ c,
                                               size_t units) {
   using W = typename A::word;
   using Gr = Groups<LOGS>;
   constexpr int N = Gr::N, TP = N / 16, PB = 256 / TP, G = Gr::G, NP = Gr::NP;
-  __shared__ W lds[PB][2][NP];
+  __shared__ W lds[PB][NTTMUL_LDS_REGIONS][NP];
 
   const int pb = threadIdx.x / TP, j = threadIdx.x % TP;
   const size_t u = (size_t)blockIdx.x * PB + pb;
   const bool live = u < units;
   const int row = L1 ? (int)(u & ((1u << L1) - 1)) : 0;
   const size_t base_g = u * N + Gr::base(0, j);
+  // threads past the batch end read unit 0 (always valid) instead of branching per load; their
+  // results are never stored
+  const size_t base_l = live ? base_g : (size_t)Gr::base(0, j);
 
   W x[16], y[16];
+#if NTTMUL_ABL_NOLOAD
 #pragma unroll
   for (int k = 0; k < 16; k++) {
-    x[k] = live ? to_word<W>(a[base_g + Gr::off(0, k)]) : W(0);
-    y[k] = live ? to_word<W>(b[base_g + Gr::off(0, k)]) : W(0);
+    x[k] = (W)(j * 16 + k + u);
+    y[k] = (W)(j * 7 + k * 3 + u);
   }
-  W *lx = lds[pb][0], *ly = lds[pb][1];
+#else
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    x[k] = to_word<W>(a[base_l + Gr::off(0, k)]);
+    y[k] = to_word<W>(b[base_l + Gr::off(0, k)]);
+  }
+#endif
+  W *lx = lds[pb][0], *ly = lds[pb][NTTMUL_LDS_REGIONS - 1];
   fwd_all<A, LOGS, 0>(P.ar, x, y, lx, ly, P.fw, j, row, L1);
 #pragma unroll
   for (int k = 0; k < 16; k++) x[k] = P.ar.mont(x[k], y[k]);
   inv_all<A, LOGS, G - 1, L1 == 0>(P, x, y, lx, ly, P.iw, j, row, L1);
+#if NTTMUL_ABL_NOSTORE
+  W acc = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) acc ^= x[k];
+  if (acc == (W)0x5A5A5A5A && live) c[base_g] = (TOut)acc;
+  return;
+#endif
   if (live) {
 #pragma unroll
     for (int k = 0; k < 16; k++) {

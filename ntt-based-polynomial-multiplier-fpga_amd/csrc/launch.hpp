@@ -13,6 +13,7 @@ struct LaunchTables {
   uint64_t q, qinv_neg;    // -q^-1 mod 2^word_bits
   uint64_t f, fs, wf, wfs; // F = n^-1 R mod q and iw[1] F, with Shoup companions
   const void *fw, *iw;     // forward / inverse twiddle pairs {w, floor(w R / q)}, n entries
+  int cus;                 // compute units of the device (persistent grid size)
 };
 
 // c = a * b for `batch` polynomials of n = 2^logn words of io_bits (32/64) each, on stream s.

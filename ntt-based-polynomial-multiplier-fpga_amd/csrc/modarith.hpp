@@ -5,7 +5,7 @@
 //
 //   Arith32 : q < 2^31, values kept in [0, 2q) inside 32-bit registers.  A twiddle product is
 //             one v_mul_hi_u32 + two v_mul_lo_u32 (Shoup, w' = floor(w 2^32 / q)); a conditional
-//             subtraction is v_sub + v_min_u32 (no compare/branch).
+//             subtraction is v_sub_co_u32 + v_cndmask_b32 (no compare/branch).
 //   Arith64 : q < 2^62, values in [0, 2q) in 64-bit registers, 64x64 Shoup via __umul64hi.
 //             Also used for 32-bit words with 2^31 <= q < 2^32 (u32 storage, u64 arithmetic).
 //
@@ -17,6 +17,12 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// conditional-subtract lowering: 0 = e32 sub_co/cndmask asm, 1 = v_min_u32,
+// 2 = __builtin_sub_overflow + select (default: measured fastest in k_rows, tools/kbench)
+#ifndef NTTMUL_CSUB
+#define NTTMUL_CSUB 2
+#endif
+
 namespace nttmul {
 
 struct Arith32 {
@@ -25,8 +31,29 @@ struct Arith32 {
   uint32_t q;
   uint32_t qinv_neg;  // -q^-1 mod 2^32
 
-  // x in [0, 2m) -> [0, m):  x - m wraps above x when x < m, so the unsigned min picks x.
-  __device__ __forceinline__ static uint32_t csub(uint32_t x, uint32_t m) { return min(x, x - m); }
+  // x in [0, 2m) -> [0, m).  Written as subtract-with-borrow + select so hipcc emits
+  // v_sub_co_u32 + v_cndmask_b32 (both full-rate on gfx950, ~2.4 cycles per wave64 instruction)
+  // instead of v_sub + v_min_u32 (v_min_u32 issues at ~4.2 cycles; tools/microbench/valu_issue).
+  __device__ __forceinline__ static uint32_t csub(uint32_t x, uint32_t m) {
+#if NTTMUL_CSUB == 1
+    return min(x, x - m);
+#elif NTTMUL_CSUB == 2
+    uint32_t d;
+    return __builtin_sub_overflow(x, m, &d) ? x : d;
+#else
+    // VOP2 (e32) forms through VCC: the VOP3 forms with an SGPR-pair carry/mask that hipcc
+    // otherwise picks issue at ~4.3 cycles each on gfx950, the e32 pair at ~2.4.  The s_nop
+    // covers the VALU-writes-VCC -> VALU-reads-VCC hazard; other waves issue meanwhile.
+    uint32_t r;
+    asm("v_subrev_co_u32_e32 %0, vcc, %2, %1\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e32 %0, %0, %1, vcc"
+        : "=&v"(r)
+        : "v"(x), "s"(m)
+        : "vcc");
+    return r;
+#endif
+  }
 
   // x * w mod q in [0, 2q) for any 32-bit x (Shoup).
   __device__ __forceinline__ uint32_t shoup(uint32_t x, uint32_t w, uint32_t ws) const {
@@ -70,8 +97,8 @@ struct Arith64 {
   uint64_t qinv_neg;  // -q^-1 mod 2^64
 
   __device__ __forceinline__ static uint64_t csub(uint64_t x, uint64_t m) {
-    uint64_t d = x - m;
-    return d < x ? d : x;  // x >= m (and m > 0) iff no wrap
+    uint64_t d;
+    return __builtin_sub_overflow(x, m, &d) ? x : d;
   }
   __device__ __forceinline__ uint64_t shoup(uint64_t x, uint64_t w, uint64_t ws) const {
     uint64_t qh = __umul64hi(x, ws);

@@ -37,6 +37,7 @@ struct DevState {
   void *io[3] = {nullptr, nullptr, nullptr};  // host-path staging for a, b, c
   size_t io_bytes = 0;
   int *flag = nullptr;                        // range-check result
+  int cus = 0;                                // compute units (persistent grid sizing)
 };
 
 }  // namespace
@@ -81,6 +82,7 @@ LaunchTables tables_for(const nttmul_ctx *ctx, const DevState &d) {
   T.f = P.f; T.fs = P.fs; T.wf = P.wf; T.wfs = P.wfs;
   T.fw = d.fw;
   T.iw = d.iw;
+  T.cus = d.cus;
   return T;
 }
 
@@ -218,7 +220,9 @@ int nttmul_create_ex(nttmul_ctx **out, const nttmul_params *prm) {
         (e = hipMalloc(&d.fw, tbytes)) != hipSuccess || (e = hipMalloc(&d.iw, tbytes)) != hipSuccess ||
         (e = hipMalloc((void **)&d.flag, sizeof(int))) != hipSuccess ||
         (e = hipMemcpy(d.fw, ctx->plan.fw.data(), tbytes, hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = hipMemcpy(d.iw, ctx->plan.iw.data(), tbytes, hipMemcpyHostToDevice)) != hipSuccess) {
+        (e = hipMemcpy(d.iw, ctx->plan.iw.data(), tbytes, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipDeviceGetAttribute(&d.cus, hipDeviceAttributeMultiprocessorCount, d.id)) !=
+            hipSuccess) {
       st = fail(ctx, e, "nttmul_create device setup");
       fprintf(stderr, "nttmul: %s\n", ctx->err);
       nttmul_destroy(ctx);

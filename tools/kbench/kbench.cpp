@@ -1,0 +1,65 @@
+// kbench — standalone timing driver for the polymul kernels (no Python, no torch), used for
+// ablation builds (-DNTTMUL_ABL_*) and quick A/B runs on the GPU box.
+//   kbench <n> <q> <batch> [reps] [io_bits]
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "launch.hpp"
+#include "planner.hpp"
+
+#define CK(x)                                                                   \
+  do {                                                                          \
+    hipError_t e = (x);                                                         \
+    if (e != hipSuccess) {                                                      \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e)); \
+      exit(1);                                                                  \
+    }                                                                           \
+  } while (0)
+
+int main(int argc, char **argv) {
+  uint32_t n = argc > 1 ? atoi(argv[1]) : 4096;
+  uint64_t q = argc > 2 ? strtoull(argv[2], 0, 0) : 2013265921ull;
+  size_t batch = argc > 3 ? strtoull(argv[3], 0, 0) : 65536;
+  int reps = argc > 4 ? atoi(argv[4]) : 20;
+  nttmul::Plan P;
+  if (nttmul::make_plan(n, q, 0, &P)) { fprintf(stderr, "bad plan\n"); return 1; }
+  int io_bits = argc > 5 ? atoi(argv[5]) : (q < (1ull << 32) ? 32 : 64);
+  size_t wb = io_bits / 8, bytes = batch * n * wb;
+  void *a, *b, *c, *fw, *iw, *scr[3] = {0, 0, 0};
+  CK(hipMalloc(&a, bytes)); CK(hipMalloc(&b, bytes)); CK(hipMalloc(&c, bytes));
+  CK(hipMalloc(&fw, P.fw.size())); CK(hipMalloc(&iw, P.iw.size()));
+  CK(hipMemcpy(fw, P.fw.data(), P.fw.size(), hipMemcpyHostToDevice));
+  CK(hipMemcpy(iw, P.iw.data(), P.iw.size(), hipMemcpyHostToDevice));
+  if (P.logn > 12)
+    for (auto &s : scr) CK(hipMalloc(&s, batch * n * (P.word_bits / 8)));
+  nttmul::LaunchTables T;
+  T.logn = P.logn; T.word_bits = P.word_bits; T.q = P.q; T.qinv_neg = P.qinv_neg;
+  T.f = P.f; T.fs = P.fs; T.wf = P.wf; T.wfs = P.wfs; T.fw = fw; T.iw = iw;
+  CK(hipDeviceGetAttribute(&T.cus, hipDeviceAttributeMultiprocessorCount, 0));
+  CK(nttmul::launch_fill(a, b, P.logn, q, 0x4E54544D554Cull, 0, batch, io_bits, 0));
+  for (int i = 0; i < 3; i++) CK(nttmul::launch_polymul(T, a, b, c, batch, io_bits, scr, 0));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  CK(hipEventRecord(e0, 0));
+  for (int i = 0; i < reps; i++) CK(nttmul::launch_polymul(T, a, b, c, batch, io_bits, scr, 0));
+  CK(hipEventRecord(e1, 0));
+  CK(hipEventSynchronize(e1));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  ms /= reps;
+  double pps = batch / (ms * 1e-3);
+  double gbs = 3.0 * n * wb * batch / (ms * 1e-3) / 1e9;
+  // checksum of c so variants can be compared for identical output
+  unsigned long long sum = 0;
+  {
+    size_t cnt = bytes / 8;
+    unsigned long long *h = (unsigned long long *)malloc(bytes);
+    CK(hipMemcpy(h, c, bytes, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < cnt; i++) sum = sum * 1099511628211ull + h[i];
+    free(h);
+  }
+  printf("%s n=%u q=%llu batch=%zu io=%d: %.4f ms  %.2f Mpolymul/s  %.1f GB/s (%.1f%% of 8 TB/s)  chk=%016llx\n",
+         VARIANT, n, (unsigned long long)q, batch, io_bits, ms, pps / 1e6, gbs, gbs / 80.0, sum);
+  return 0;
+}

@@ -1,0 +1,61 @@
+"""Summarise a tools/gpu_round.sh output directory into profiles/ (committed evidence).
+
+    python tools/summarize_profile.py gpurun_out/<tag> profiles/<round>
+
+Writes <round>_kernel_stats.csv (rocprofv3 --kernel-trace --stats of bench.py), <round>_pmc.json
+(per-dispatch counter averages of the dominant kernel) and updates profiles/pmc_traffic.json, the
+HBM-bytes-per-launch table bench.py reads for roofline.traffic.  FETCH_SIZE is doubled per
+MI355X_MICROARCH.md §HBM (gfx950 reports half the bytes of coalesced streaming reads; checked on
+this kernel: 2 x FETCH_SIZE = the 2 GiB of a and b it reads, within 0.05 %); WRITE_SIZE is exact.
+"""
+import csv
+import collections
+import json
+import os
+import shutil
+import sys
+
+src, dst = sys.argv[1], sys.argv[2]
+os.makedirs(os.path.dirname(dst) or ".", exist_ok=True)
+shutil.copy(os.path.join(src, "trace", "trace_kernel_stats.csv"), dst + "_kernel_stats.csv")
+bench = json.loads(open(os.path.join(src, "bench.json")).read().strip().splitlines()[-1])
+shutil.copy(os.path.join(src, "bench.json"), dst + "_bench.json")
+
+pmc = collections.defaultdict(list)
+dur = collections.defaultdict(list)
+for root, _, files in os.walk(os.path.join(src, "pmc")):
+    for f in files:
+        if not f.endswith("_counter_collection.csv"):
+            continue
+        for r in csv.DictReader(open(os.path.join(root, f))):
+            k = r["Kernel_Name"]
+            pmc[(k, r["Counter_Name"])].append(float(r["Counter_Value"]))
+            dur[k].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+out = {}
+for (k, c), v in sorted(pmc.items()):
+    out.setdefault(k, {})[c] = sum(v) / len(v)
+for k in out:
+    out[k]["profiled_duration_ns_avg"] = sum(dur[k]) / len(dur[k])
+json.dump(out, open(dst + "_pmc.json", "w"), indent=1)
+
+cfg = bench["config"]
+main = "k_rows" if "k_rows" in out else sorted(out)[0]
+m = out[main]
+fetch = 2.0 * m["FETCH_SIZE"] * 1024
+write = m["WRITE_SIZE"] * 1024
+tpath = os.path.join(os.path.dirname(dst) or ".", "pmc_traffic.json")
+table = json.load(open(tpath)) if os.path.exists(tpath) else {"entries": []}
+table["entries"] = [e for e in table["entries"]
+                    if not (e["n"] == cfg["n"] and e["q"] == cfg["q"] and e["batch"] == cfg["batch_per_gpu"])]
+entry = {"n": cfg["n"], "q": cfg["q"], "batch": cfg["batch_per_gpu"], "kernel": main,
+         "hbm_bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
+         "alg_bytes_per_launch": bench["roofline"]["alg_bytes_per_launch"],
+         "traffic_over_alg": (fetch + write) / bench["roofline"]["alg_bytes_per_launch"],
+         "source": os.path.basename(dst) + "_pmc.json",
+         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; "
+                   "KB x 1024; FETCH_SIZE x 2 (gfx950 half-count of coalesced reads)"}
+if "GRBM_GUI_ACTIVE" in m:
+    entry["clock_ghz"] = m["GRBM_GUI_ACTIVE"] / 8 / m["profiled_duration_ns_avg"]
+table["entries"].append(entry)
+json.dump(table, open(tpath, "w"), indent=1)
+print(json.dumps(entry, indent=1))
