@@ -96,6 +96,31 @@ int nttmul_multiply_batch_u64(nttmul_ctx *ctx, uint64_t *c, const uint64_t *a, c
 int nttmul_multiply_batch_device(nttmul_ctx *ctx, void *c, const void *a, const void *b,
                                  size_t batch, int word_bits, int dev, void *stream);
 
+/* Standalone transforms, so a caller can keep operands in the NTT domain:
+ *   forward  = mulntt_ct_std2rev (NTT/ntt.C:342-371; ≙ mul_array16(psi_powers) followed by
+ *              ntt_ct_std2rev, the first two steps of ntt256_product1): negacyclic NTT, standard
+ *              order in, bit-reversed order out, canonical [0, q).  Equal, element for element,
+ *              to the reference's a[] after those two steps.
+ *   inverse  = nttmul_gs_rev2std (NTT/ntt.C:428-451) followed by the n^-1 scaling of
+ *              ntt256.C:12: bit-reversed in, standard out; inverse(forward(a)) == a.  (The
+ *              reference's unscaled inttmul256_gs_rev2std output is n times this.)
+ *   pointwise = mul_array (NTT/ntt.C:131-137): c[i] = a[i] * b[i] mod q, canonical.
+ * Host-buffer forms take [batch][n] arrays; device forms as nttmul_multiply_batch_device. */
+int nttmul_forward_batch_u32(nttmul_ctx *ctx, uint32_t *out, const uint32_t *in, size_t batch);
+int nttmul_forward_batch_u64(nttmul_ctx *ctx, uint64_t *out, const uint64_t *in, size_t batch);
+int nttmul_inverse_batch_u32(nttmul_ctx *ctx, uint32_t *out, const uint32_t *in, size_t batch);
+int nttmul_inverse_batch_u64(nttmul_ctx *ctx, uint64_t *out, const uint64_t *in, size_t batch);
+int nttmul_pointwise_batch_u32(nttmul_ctx *ctx, uint32_t *c, const uint32_t *a,
+                               const uint32_t *b, size_t batch);
+int nttmul_pointwise_batch_u64(nttmul_ctx *ctx, uint64_t *c, const uint64_t *a,
+                               const uint64_t *b, size_t batch);
+int nttmul_forward_batch_device(nttmul_ctx *ctx, void *out, const void *in, size_t batch,
+                                int word_bits, int dev, void *stream);
+int nttmul_inverse_batch_device(nttmul_ctx *ctx, void *out, const void *in, size_t batch,
+                                int word_bits, int dev, void *stream);
+int nttmul_pointwise_batch_device(nttmul_ctx *ctx, void *c, const void *a, const void *b,
+                                  size_t batch, int word_bits, int dev, void *stream);
+
 /* Synthetic inputs on the device: a[p][i] = splitmix64(seed + 2n(p0+p) + i) mod q,
  * b[p][i] = splitmix64(seed + 2n(p0+p) + n + i) mod q, for p in [0, count).  Asynchronous. */
 int nttmul_fill_random_device(nttmul_ctx *ctx, void *a, void *b, uint64_t p0, size_t count,

@@ -101,8 +101,8 @@ struct Groups {
 template <class W, class T>
 __device__ __forceinline__ W to_word(T v) { return (W)v; }
 
-// Forward CT stages of group g on two polynomials (same twiddles).
-template <class A, int LOGS, int g>
+// Forward CT stages of group g on NPOLY (1 or 2) polynomials (same twiddles).
+template <class A, int LOGS, int g, int NPOLY = 2>
 __device__ __forceinline__ void fwd_group(const A &ar, typename A::word (&x)[16],
                                           typename A::word (&y)[16],
                                           const TwPair<typename A::word> *__restrict__ tw, int j,
@@ -121,7 +121,7 @@ __device__ __forceinline__ void fwd_group(const A &ar, typename A::word (&x)[16]
       const int idx = tbase + (Gr::blk(g, j, k) << l) + (m >> (S - l));
       const TwPair<typename A::word> t = tw[idx];
       ar.ct(x[k], x[k + dist], t.w, t.ws);
-      ar.ct(y[k], y[k + dist], t.w, t.ws);
+      if (NPOLY == 2) ar.ct(y[k], y[k + dist], t.w, t.ws);
     }
   }
 }
@@ -191,17 +191,17 @@ __device__ __forceinline__ void exchange(W (&x)[16], W (&y)[16], W *lds_x, W *ld
   __syncthreads();
 }
 
-template <class A, int LOGS, int g>
+template <class A, int LOGS, int g, int NPOLY = 2>
 __device__ __forceinline__ void fwd_all(const A &ar, typename A::word (&x)[16],
                                         typename A::word (&y)[16], typename A::word *lx,
                                         typename A::word *ly,
                                         const TwPair<typename A::word> *__restrict__ tw, int j,
                                         int row, int l1) {
   using Gr = Groups<LOGS>;
-  fwd_group<A, LOGS, g>(ar, x, y, tw, j, row, l1);
+  fwd_group<A, LOGS, g, NPOLY>(ar, x, y, tw, j, row, l1);
   if constexpr (g + 1 < Gr::G) {
-    exchange<LOGS, g, g + 1, 2>(x, y, lx, ly, j);
-    fwd_all<A, LOGS, g + 1>(ar, x, y, lx, ly, tw, j, row, l1);
+    exchange<LOGS, g, g + 1, NPOLY>(x, y, lx, ly, j);
+    fwd_all<A, LOGS, g + 1, NPOLY>(ar, x, y, lx, ly, tw, j, row, l1);
   }
 }
 
@@ -276,9 +276,60 @@ __global__ __launch_bounds__(256, NTTMUL_MIN_WAVES) void k_rows(KParams<A> P, co
   }
 }
 
+// Standalone transforms, one polynomial per unit of 2^LOGS coefficients.
+//   DIR 0 (forward): NTT/ntt.C:342-371 mulntt_ct_std2rev — standard order in, bit-reversed out;
+//     with L1 > 0 this is the row pass after k_cols_fwd.  Output canonical when L1 == 0 or
+//     the row pass is the last forward step (always, for the forward direction).
+//   DIR 1 (inverse): NTT/ntt.C:428-451 nttmul_gs_rev2std followed by the n^-1 scaling of
+//     ntt256.C:12 (P.f = n^-1 here), so inverse(forward(a)) == a; with L1 > 0 this is the row
+//     pass before k_cols_inv and the output stays lazy.
+template <class A, class TIn, class TOut, int LOGS, int L1, int DIR>
+__global__ __launch_bounds__(256) void k_xform(KParams<A> P, const TIn *__restrict__ in,
+                                               TOut *__restrict__ out, size_t units) {
+  using W = typename A::word;
+  using Gr = Groups<LOGS>;
+  constexpr int N = Gr::N, TP = N / 16, PB = 256 / TP, G = Gr::G, NP = Gr::NP;
+  constexpr int GIN = DIR == 0 ? 0 : G - 1, GOUT = DIR == 0 ? G - 1 : 0;
+  __shared__ W lds[PB][NP];
+  const int pb = threadIdx.x / TP, j = threadIdx.x % TP;
+  const size_t u = (size_t)blockIdx.x * PB + pb;
+  const bool live = u < units;
+  const int row = L1 ? (int)(u & ((1u << L1) - 1)) : 0;
+  const size_t base_in = (live ? u : 0) * N + Gr::base(GIN, j);
+  W x[16], y[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) x[k] = to_word<W>(in[base_in + Gr::off(GIN, k)]);
+  if (DIR == 0)
+    fwd_all<A, LOGS, 0, 1>(P.ar, x, y, lds[pb], lds[pb], P.fw, j, row, L1);
+  else
+    inv_all<A, LOGS, G - 1, L1 == 0>(P, x, y, lds[pb], lds[pb], P.iw, j, row, L1);
+  if (live) {
+    const size_t base_out = u * N + Gr::base(GOUT, j);
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      W v = x[k];
+      if (DIR == 0 || L1 == 0) v = P.ar.canon(v);
+      out[base_out + Gr::off(GOUT, k)] = (TOut)v;
+    }
+  }
+}
+
+// c = a * b mod q coefficient-wise (NTT/ntt.C:131-137 mul_array), canonical in and out:
+// two Montgomery products, the second by R^2 mod q (P.f holds R^2 mod q for this kernel).
+template <class A, class IO>
+__global__ __launch_bounds__(256) void k_pointwise(KParams<A> P, const IO *__restrict__ a,
+                                                   const IO *__restrict__ b, IO *__restrict__ c,
+                                                   size_t total) {
+  using W = typename A::word;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const W t = P.ar.mont((W)a[i], (W)b[i]);
+  c[i] = (IO)P.ar.canon(P.ar.mont(t, P.f));
+}
+
 // Column pass, forward: global stages 0..L1-1 of CT on a and b.  Thread = one column
 // (e = col + m * 2^LOGS, m < 2^L1); lanes on consecutive columns -> coalesced rows.
-template <class A, class TIn, int L1>
+template <class A, class TIn, int L1, int NPOLY = 2>
 __global__ __launch_bounds__(256) void k_cols_fwd(KParams<A> P, const TIn *__restrict__ a,
                                                   const TIn *__restrict__ b,
                                                   typename A::word *__restrict__ ta,
@@ -295,7 +346,7 @@ __global__ __launch_bounds__(256) void k_cols_fwd(KParams<A> P, const TIn *__res
 #pragma unroll
   for (int m = 0; m < M; m++) {
     x[m] = (W)a[base + ((size_t)m << logs)];
-    y[m] = (W)b[base + ((size_t)m << logs)];
+    y[m] = NPOLY == 2 ? (W)b[base + ((size_t)m << logs)] : W(0);
   }
 #pragma unroll
   for (int st = 0; st < L1; st++) {
@@ -305,13 +356,13 @@ __global__ __launch_bounds__(256) void k_cols_fwd(KParams<A> P, const TIn *__res
       if (m & dist) continue;
       const TwPair<W> t = P.fw[(1 << st) + (m >> (L1 - st))];
       P.ar.ct(x[m], x[m + dist], t.w, t.ws);
-      P.ar.ct(y[m], y[m + dist], t.w, t.ws);
+      if (NPOLY == 2) P.ar.ct(y[m], y[m + dist], t.w, t.ws);
     }
   }
 #pragma unroll
   for (int m = 0; m < M; m++) {
     ta[base + ((size_t)m << logs)] = x[m];
-    tb[base + ((size_t)m << logs)] = y[m];
+    if (NPOLY == 2) tb[base + ((size_t)m << logs)] = y[m];
   }
 }
 
@@ -465,6 +516,114 @@ hipError_t launch_polymul(const LaunchTables &T, const void *a, const void *b, v
                : fused<Arith64, uint32_t>(T, a, b, c, batch, s);
   return big ? multipass<Arith64, uint64_t>(T, a, b, c, batch, scr, s)
              : fused<Arith64, uint64_t>(T, a, b, c, batch, s);
+}
+
+template <class A, class TIn, class TOut, int LOGS, int L1, int DIR>
+static hipError_t launch_xform_rows(const KParams<A> &P, const void *in, void *out, size_t units,
+                                    hipStream_t s) {
+  constexpr int PB = 256 / ((1 << LOGS) / 16);
+  const size_t blocks = (units + PB - 1) / PB;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL((k_xform<A, TIn, TOut, LOGS, L1, DIR>), dim3((unsigned)blocks), dim3(256), 0,
+                     s, P, (const TIn *)in, (TOut *)out, units);
+  return hipGetLastError();
+}
+
+// KParams for the standalone inverse: scale by n^-1 only (no Montgomery factor)
+template <class A>
+static KParams<A> inverse_params(const LaunchTables &T) {
+  KParams<A> P = make_params<A>(T);
+  P.f = (typename A::word)T.fi; P.fs = (typename A::word)T.fis;
+  P.wf = (typename A::word)T.wfi; P.wfs = (typename A::word)T.wfis;
+  return P;
+}
+
+template <class A, class IO, int DIR>
+static hipError_t xform_fused(const LaunchTables &T, const void *in, void *out, size_t batch,
+                              hipStream_t s) {
+  const KParams<A> P = DIR == 0 ? make_params<A>(T) : inverse_params<A>(T);
+  switch (T.logn) {
+    case 8: return launch_xform_rows<A, IO, IO, 8, 0, DIR>(P, in, out, batch, s);
+    case 9: return launch_xform_rows<A, IO, IO, 9, 0, DIR>(P, in, out, batch, s);
+    case 10: return launch_xform_rows<A, IO, IO, 10, 0, DIR>(P, in, out, batch, s);
+    case 11: return launch_xform_rows<A, IO, IO, 11, 0, DIR>(P, in, out, batch, s);
+    case 12: return launch_xform_rows<A, IO, IO, 12, 0, DIR>(P, in, out, batch, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <class A, class IO, int L1, int DIR>
+static hipError_t xform_multipass_l1(const LaunchTables &T, const void *in, void *out,
+                                     size_t batch, void **scr, hipStream_t s) {
+  using W = typename A::word;
+  constexpr int LOGS = 12;
+  const size_t cols = batch << LOGS;
+  const unsigned cblocks = (unsigned)((cols + 255) / 256);
+  if (DIR == 0) {
+    const KParams<A> P = make_params<A>(T);
+    hipLaunchKernelGGL((k_cols_fwd<A, IO, L1, 1>), dim3(cblocks), dim3(256), 0, s, P,
+                       (const IO *)in, (const IO *)nullptr, (W *)scr[0], (W *)nullptr, batch,
+                       LOGS);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return launch_xform_rows<A, W, IO, LOGS, L1, 0>(P, scr[0], out, batch << L1, s);
+  }
+  const KParams<A> P = inverse_params<A>(T);
+  hipError_t e = launch_xform_rows<A, IO, W, LOGS, L1, 1>(P, in, scr[0], batch << L1, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((k_cols_inv<A, IO, L1>), dim3(cblocks), dim3(256), 0, s, P,
+                     (const W *)scr[0], (IO *)out, batch, LOGS);
+  return hipGetLastError();
+}
+
+template <class A, class IO, int DIR>
+static hipError_t xform_any(const LaunchTables &T, const void *in, void *out, size_t batch,
+                            void **scr, hipStream_t s) {
+  switch (T.logn) {
+    case 13: return xform_multipass_l1<A, IO, 1, DIR>(T, in, out, batch, scr, s);
+    case 14: return xform_multipass_l1<A, IO, 2, DIR>(T, in, out, batch, scr, s);
+    case 15: return xform_multipass_l1<A, IO, 3, DIR>(T, in, out, batch, scr, s);
+    case 16: return xform_multipass_l1<A, IO, 4, DIR>(T, in, out, batch, scr, s);
+    default: return xform_fused<A, IO, DIR>(T, in, out, batch, s);
+  }
+}
+
+template <int DIR>
+static hipError_t launch_xform_dir(const LaunchTables &T, const void *in, void *out, size_t batch,
+                                   int io_bits, void **scr, hipStream_t s) {
+  if (T.word_bits == 32)
+    return io_bits == 64 ? xform_any<Arith32, uint64_t, DIR>(T, in, out, batch, scr, s)
+                         : xform_any<Arith32, uint32_t, DIR>(T, in, out, batch, scr, s);
+  return io_bits == 64 ? xform_any<Arith64, uint64_t, DIR>(T, in, out, batch, scr, s)
+                       : xform_any<Arith64, uint32_t, DIR>(T, in, out, batch, scr, s);
+}
+
+hipError_t launch_xform(const LaunchTables &T, const void *in, void *out, size_t batch,
+                        int io_bits, int inverse, void **scr, hipStream_t s) {
+  return inverse ? launch_xform_dir<1>(T, in, out, batch, io_bits, scr, s)
+                 : launch_xform_dir<0>(T, in, out, batch, io_bits, scr, s);
+}
+
+template <class A, class IO>
+static hipError_t pointwise(const LaunchTables &T, const void *a, const void *b, void *c,
+                            size_t total, hipStream_t s) {
+  KParams<A> P = make_params<A>(T);
+  P.f = (typename A::word)T.r2;
+  const unsigned blocks = (unsigned)((total + 255) / 256);
+  hipLaunchKernelGGL((k_pointwise<A, IO>), dim3(blocks), dim3(256), 0, s, P, (const IO *)a,
+                     (const IO *)b, (IO *)c, total);
+  return hipGetLastError();
+}
+
+hipError_t launch_pointwise(const LaunchTables &T, const void *a, const void *b, void *c,
+                            size_t batch, int io_bits, hipStream_t s) {
+  const size_t total = batch << T.logn;
+  if (!total) return hipSuccess;
+  if (T.word_bits == 32)
+    return io_bits == 64 ? pointwise<Arith32, uint64_t>(T, a, b, c, total, s)
+                         : pointwise<Arith32, uint32_t>(T, a, b, c, total, s);
+  return io_bits == 64 ? pointwise<Arith64, uint64_t>(T, a, b, c, total, s)
+                       : pointwise<Arith64, uint32_t>(T, a, b, c, total, s);
 }
 
 hipError_t launch_fill(void *a, void *b, uint32_t logn, uint64_t q, uint64_t seed, uint64_t p0,

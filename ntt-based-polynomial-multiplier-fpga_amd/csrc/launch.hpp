@@ -12,6 +12,8 @@ struct LaunchTables {
   int word_bits;           // 32 -> Arith32 (q < 2^31), 64 -> Arith64
   uint64_t q, qinv_neg;    // -q^-1 mod 2^word_bits
   uint64_t f, fs, wf, wfs; // F = n^-1 R mod q and iw[1] F, with Shoup companions
+  uint64_t fi, fis, wfi, wfis; // n^-1 and iw[1] n^-1 (standalone inverse), with companions
+  uint64_t r2;             // R^2 mod q (standalone pointwise product)
   const void *fw, *iw;     // forward / inverse twiddle pairs {w, floor(w R / q)}, n entries
   int cus;                 // compute units of the device (persistent grid size)
 };
@@ -20,6 +22,13 @@ struct LaunchTables {
 // scr: three device buffers of batch * n words of word_bits, used only when n > 4096.
 hipError_t launch_polymul(const LaunchTables &T, const void *a, const void *b, void *c,
                           size_t batch, int io_bits, void **scr, hipStream_t s);
+// Standalone forward (inverse = 0) or inverse (inverse = 1) NTT of `batch` polynomials
+// (SURVEY §8f row 1).  scr as for launch_polymul (only scr[0] is used).
+hipError_t launch_xform(const LaunchTables &T, const void *in, void *out, size_t batch,
+                        int io_bits, int inverse, void **scr, hipStream_t s);
+// c = a * b mod q coefficient-wise over batch * n words.
+hipError_t launch_pointwise(const LaunchTables &T, const void *a, const void *b, void *c,
+                            size_t batch, int io_bits, hipStream_t s);
 hipError_t launch_fill(void *a, void *b, uint32_t logn, uint64_t q, uint64_t seed, uint64_t p0,
                        size_t count, int io_bits, hipStream_t s);
 hipError_t launch_check_range(const void *a, const void *b, uint64_t q, size_t total, int io_bits,

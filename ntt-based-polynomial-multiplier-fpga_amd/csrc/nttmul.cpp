@@ -80,6 +80,7 @@ LaunchTables tables_for(const nttmul_ctx *ctx, const DevState &d) {
   T.q = P.q;
   T.qinv_neg = P.qinv_neg;
   T.f = P.f; T.fs = P.fs; T.wf = P.wf; T.wfs = P.wfs;
+  T.fi = P.fi; T.fis = P.fis; T.wfi = P.wfi; T.wfis = P.wfis; T.r2 = P.r2;
   T.fw = d.fw;
   T.iw = d.iw;
   T.cus = d.cus;
@@ -104,16 +105,20 @@ int ensure(nttmul_ctx *ctx, void **bufs, int nb, size_t *have, size_t need) {
   return NTTMUL_OK;
 }
 
-// Enqueue one device-resident batch on d (current device must be d.id).
-int run_device(nttmul_ctx *ctx, DevState &d, void *c, const void *a, const void *b, size_t batch,
-               int io_bits, hipStream_t s) {
+enum Op { OP_MULTIPLY = 0, OP_FORWARD = 1, OP_INVERSE = 2, OP_POINTWISE = 3 };
+
+// Enqueue one device-resident batch of `op` on d (current device must be d.id).  b is unused by
+// the transforms.
+int run_device(nttmul_ctx *ctx, DevState &d, int op, void *c, const void *a, const void *b,
+               size_t batch, int io_bits, hipStream_t s) {
   const Plan &P = ctx->plan;
   if (!batch) return NTTMUL_OK;
   if (io_bits != 32 && io_bits != 64) return NTTMUL_EINVAL;
   if (io_bits == 32 && P.q > 0xFFFFFFFFull) return NTTMUL_EINVAL;  // q does not fit the words
   if (ctx->flags & NTTMUL_FLAG_VALIDATE) {
     HIP_TRY(ctx, hipMemsetAsync(d.flag, 0, sizeof(int), s));
-    HIP_TRY(ctx, launch_check_range(a, b, P.q, batch * P.n, io_bits, d.flag, s));
+    HIP_TRY(ctx, launch_check_range(a, (op == OP_MULTIPLY || op == OP_POINTWISE) ? b : a, P.q,
+                                    batch * P.n, io_bits, d.flag, s));
     int bad = 0;
     HIP_TRY(ctx, hipMemcpyAsync(&bad, d.flag, sizeof(int), hipMemcpyDeviceToHost, s));
     HIP_TRY(ctx, hipStreamSynchronize(s));
@@ -128,13 +133,20 @@ int run_device(nttmul_ctx *ctx, DevState &d, void *c, const void *a, const void 
     if (st) return st;
   }
   const LaunchTables T = tables_for(ctx, d);
-  HIP_TRY(ctx, launch_polymul(T, a, b, c, batch, io_bits, d.scr, s));
+  switch (op) {
+    case OP_MULTIPLY: HIP_TRY(ctx, launch_polymul(T, a, b, c, batch, io_bits, d.scr, s)); break;
+    case OP_FORWARD: HIP_TRY(ctx, launch_xform(T, a, c, batch, io_bits, 0, d.scr, s)); break;
+    case OP_INVERSE: HIP_TRY(ctx, launch_xform(T, a, c, batch, io_bits, 1, d.scr, s)); break;
+    case OP_POINTWISE: HIP_TRY(ctx, launch_pointwise(T, a, b, c, batch, io_bits, s)); break;
+    default: return NTTMUL_EINVAL;
+  }
   return NTTMUL_OK;
 }
 
-int multiply_host(nttmul_ctx *ctx, void *c, const void *a, const void *b, size_t batch,
-                  int io_bits) {
-  if (!ctx || !c || !a || !b) return NTTMUL_EINVAL;
+int run_host(nttmul_ctx *ctx, int op, void *c, const void *a, const void *b, size_t batch,
+             int io_bits) {
+  const bool two = op == OP_MULTIPLY || op == OP_POINTWISE;
+  if (!ctx || !c || !a || (two && !b)) return NTTMUL_EINVAL;
   if (!batch) return NTTMUL_OK;
   DeviceGuard guard;
   const size_t wb = io_bits / 8, n = ctx->plan.n;
@@ -151,9 +163,10 @@ int multiply_host(nttmul_ctx *ctx, void *c, const void *a, const void *b, size_t
       const size_t off = p0 * n * wb, bytes = cnt * n * wb;
       HIP_TRY(ctx, hipMemcpyAsync(d.io[0], (const char *)a + off, bytes, hipMemcpyHostToDevice,
                                   d.stream));
-      HIP_TRY(ctx, hipMemcpyAsync(d.io[1], (const char *)b + off, bytes, hipMemcpyHostToDevice,
-                                  d.stream));
-      st = run_device(ctx, d, d.io[2], d.io[0], d.io[1], cnt, io_bits, d.stream);
+      if (two)
+        HIP_TRY(ctx, hipMemcpyAsync(d.io[1], (const char *)b + off, bytes,
+                                    hipMemcpyHostToDevice, d.stream));
+      st = run_device(ctx, d, op, d.io[2], d.io[0], d.io[1], cnt, io_bits, d.stream);
       if (st) return st;
       HIP_TRY(ctx, hipMemcpyAsync((char *)c + off, d.io[2], bytes, hipMemcpyDeviceToHost,
                                   d.stream));
@@ -277,27 +290,65 @@ int nttmul_get_info(const nttmul_ctx *ctx, nttmul_info *info) {
 
 int nttmul_multiply_batch_u32(nttmul_ctx *ctx, uint32_t *c, const uint32_t *a, const uint32_t *b,
                               size_t batch) {
-  return multiply_host(ctx, c, a, b, batch, 32);
+  return run_host(ctx, OP_MULTIPLY, c, a, b, batch, 32);
 }
 int nttmul_multiply_batch_u64(nttmul_ctx *ctx, uint64_t *c, const uint64_t *a, const uint64_t *b,
                               size_t batch) {
-  return multiply_host(ctx, c, a, b, batch, 64);
+  return run_host(ctx, OP_MULTIPLY, c, a, b, batch, 64);
 }
 int nttmul_multiply_u32(nttmul_ctx *ctx, uint32_t *c, const uint32_t *a, const uint32_t *b) {
-  return multiply_host(ctx, c, a, b, 1, 32);
+  return run_host(ctx, OP_MULTIPLY, c, a, b, 1, 32);
 }
 int nttmul_multiply_u64(nttmul_ctx *ctx, uint64_t *c, const uint64_t *a, const uint64_t *b) {
-  return multiply_host(ctx, c, a, b, 1, 64);
+  return run_host(ctx, OP_MULTIPLY, c, a, b, 1, 64);
+}
+int nttmul_forward_batch_u32(nttmul_ctx *ctx, uint32_t *out, const uint32_t *in, size_t batch) {
+  return run_host(ctx, OP_FORWARD, out, in, nullptr, batch, 32);
+}
+int nttmul_forward_batch_u64(nttmul_ctx *ctx, uint64_t *out, const uint64_t *in, size_t batch) {
+  return run_host(ctx, OP_FORWARD, out, in, nullptr, batch, 64);
+}
+int nttmul_inverse_batch_u32(nttmul_ctx *ctx, uint32_t *out, const uint32_t *in, size_t batch) {
+  return run_host(ctx, OP_INVERSE, out, in, nullptr, batch, 32);
+}
+int nttmul_inverse_batch_u64(nttmul_ctx *ctx, uint64_t *out, const uint64_t *in, size_t batch) {
+  return run_host(ctx, OP_INVERSE, out, in, nullptr, batch, 64);
+}
+int nttmul_pointwise_batch_u32(nttmul_ctx *ctx, uint32_t *c, const uint32_t *a,
+                               const uint32_t *b, size_t batch) {
+  return run_host(ctx, OP_POINTWISE, c, a, b, batch, 32);
+}
+int nttmul_pointwise_batch_u64(nttmul_ctx *ctx, uint64_t *c, const uint64_t *a,
+                               const uint64_t *b, size_t batch) {
+  return run_host(ctx, OP_POINTWISE, c, a, b, batch, 64);
 }
 
-int nttmul_multiply_batch_device(nttmul_ctx *ctx, void *c, const void *a, const void *b,
-                                 size_t batch, int word_bits, int dev, void *stream) {
-  if (!ctx || (batch && (!c || !a || !b))) return NTTMUL_EINVAL;
+static int device_op(nttmul_ctx *ctx, int op, void *c, const void *a, const void *b, size_t batch,
+                     int word_bits, int dev, void *stream) {
+  const bool two = op == OP_MULTIPLY || op == OP_POINTWISE;
+  if (!ctx || (batch && (!c || !a || (two && !b)))) return NTTMUL_EINVAL;
   DevState *d = find_dev(ctx, dev);
   if (!d) return NTTMUL_ENODEV;
   DeviceGuard guard;
   HIP_TRY(ctx, hipSetDevice(d->id));
-  return run_device(ctx, *d, c, a, b, batch, word_bits, (hipStream_t)stream);
+  return run_device(ctx, *d, op, c, a, b, batch, word_bits, (hipStream_t)stream);
+}
+
+int nttmul_multiply_batch_device(nttmul_ctx *ctx, void *c, const void *a, const void *b,
+                                 size_t batch, int word_bits, int dev, void *stream) {
+  return device_op(ctx, OP_MULTIPLY, c, a, b, batch, word_bits, dev, stream);
+}
+int nttmul_forward_batch_device(nttmul_ctx *ctx, void *out, const void *in, size_t batch,
+                                int word_bits, int dev, void *stream) {
+  return device_op(ctx, OP_FORWARD, out, in, nullptr, batch, word_bits, dev, stream);
+}
+int nttmul_inverse_batch_device(nttmul_ctx *ctx, void *out, const void *in, size_t batch,
+                                int word_bits, int dev, void *stream) {
+  return device_op(ctx, OP_INVERSE, out, in, nullptr, batch, word_bits, dev, stream);
+}
+int nttmul_pointwise_batch_device(nttmul_ctx *ctx, void *c, const void *a, const void *b,
+                                  size_t batch, int word_bits, int dev, void *stream) {
+  return device_op(ctx, OP_POINTWISE, c, a, b, batch, word_bits, dev, stream);
 }
 
 int nttmul_fill_random_device(nttmul_ctx *ctx, void *a, void *b, uint64_t p0, size_t count,

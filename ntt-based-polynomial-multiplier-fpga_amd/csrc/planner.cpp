@@ -136,6 +136,12 @@ int make_plan(uint32_t n, uint64_t q, uint64_t psi, Plan *P) {
   P->fs = companion(P->f, q, bits);
   P->wf = mulmod(iw[1], P->f, q);
   P->wfs = companion(P->wf, q, bits);
+  // standalone inverse NTT: plain n^-1 (ntt256.C:12); pointwise product: R^2 mod q
+  P->fi = P->inv_n;
+  P->fis = companion(P->fi, q, bits);
+  P->wfi = mulmod(iw[1], P->fi, q);
+  P->wfis = companion(P->wfi, q, bits);
+  P->r2 = mulmod(r_mod_q, r_mod_q, q);
   return NTTMUL_OK;
 }
 

@@ -24,6 +24,7 @@ struct Plan {
   uint64_t q = 0, psi = 0, omega = 0, inv_psi = 0, inv_omega = 0, inv_n = 0;
   int word_bits = 0;                 // 32 when q < 2^31 (lazy [0, 2q) fits a u32), else 64
   uint64_t qinv_neg = 0, f = 0, fs = 0, wf = 0, wfs = 0;
+  uint64_t fi = 0, fis = 0, wfi = 0, wfis = 0, r2 = 0;  // standalone inverse / pointwise
   // interleaved {w, w'} pairs (u32 or u64 each), n entries; entry 0 unused
   std::vector<uint8_t> fw, iw;
 };

@@ -76,6 +76,13 @@ def load_library() -> ctypes.CDLL:
     for name in ("nttmul_multiply_batch_u32", "nttmul_multiply_batch_u64"):
         getattr(lib, name).argtypes = [vp, vp, vp, vp, sz]
     lib.nttmul_multiply_batch_device.argtypes = [vp, vp, vp, vp, sz, i32, i32, vp]
+    for op in ("forward", "inverse"):
+        for w in ("u32", "u64"):
+            getattr(lib, f"nttmul_{op}_batch_{w}").argtypes = [vp, vp, vp, sz]
+        getattr(lib, f"nttmul_{op}_batch_device").argtypes = [vp, vp, vp, sz, i32, i32, vp]
+    for w in ("u32", "u64"):
+        getattr(lib, f"nttmul_pointwise_batch_{w}").argtypes = [vp, vp, vp, vp, sz]
+    lib.nttmul_pointwise_batch_device.argtypes = [vp, vp, vp, vp, sz, i32, i32, vp]
     lib.nttmul_fill_random_device.argtypes = [vp, vp, vp, u64, sz, u64, i32, i32, vp]
     for name in ("ntt256_product1", "ntt256_product4", "ntt_red256_product1", "ntt_red256_product4"):
         getattr(lib, name).argtypes = [vp, vp, vp]
@@ -162,6 +169,54 @@ class Context:
         fn = self._lib.nttmul_multiply_batch_u32 if dtype == np.uint32 else self._lib.nttmul_multiply_batch_u64
         self._check(fn(self._h, c.ctypes.data, a.ctypes.data, b.ctypes.data, batch))
         return c
+
+    def _unary(self, op: str, x, dtype=None) -> np.ndarray:
+        dtype = dtype or self.io_dtype
+        x = np.ascontiguousarray(x, dtype=dtype)
+        if x.shape[-1] != self.n:
+            raise ValueError("input must have shape [..., n]")
+        out = np.empty_like(x)
+        w = "u32" if dtype == np.uint32 else "u64"
+        fn = getattr(self._lib, f"nttmul_{op}_batch_{w}")
+        self._check(fn(self._h, out.ctypes.data, x.ctypes.data, x.size // self.n))
+        return out
+
+    def forward(self, a, dtype=None) -> np.ndarray:
+        """Negacyclic forward NTT, bit-reversed output (NTT/ntt.C:342 mulntt_ct_std2rev)."""
+        return self._unary("forward", a, dtype)
+
+    def inverse(self, a_hat, dtype=None) -> np.ndarray:
+        """Inverse of forward(): nttmul_gs_rev2std (NTT/ntt.C:428) then n^-1."""
+        return self._unary("inverse", a_hat, dtype)
+
+    def pointwise(self, a, b, dtype=None) -> np.ndarray:
+        """c[i] = a[i] * b[i] mod q (NTT/ntt.C:131 mul_array)."""
+        dtype = dtype or self.io_dtype
+        a = np.ascontiguousarray(a, dtype=dtype)
+        b = np.ascontiguousarray(b, dtype=dtype)
+        c = np.empty_like(a)
+        w = "u32" if dtype == np.uint32 else "u64"
+        fn = getattr(self._lib, f"nttmul_pointwise_batch_{w}")
+        self._check(fn(self._h, c.ctypes.data, a.ctypes.data, b.ctypes.data, a.size // self.n))
+        return c
+
+    def forward_device(self, out, a, batch: int, word_bits: int, dev: Optional[int] = None,
+                       stream: int = 0):
+        dev = self.first_dev if dev is None else dev
+        self._check(self._lib.nttmul_forward_batch_device(self._h, _ptr(out), _ptr(a), batch,
+                                                          word_bits, dev, stream or None))
+
+    def inverse_device(self, out, a, batch: int, word_bits: int, dev: Optional[int] = None,
+                       stream: int = 0):
+        dev = self.first_dev if dev is None else dev
+        self._check(self._lib.nttmul_inverse_batch_device(self._h, _ptr(out), _ptr(a), batch,
+                                                          word_bits, dev, stream or None))
+
+    def pointwise_device(self, c, a, b, batch: int, word_bits: int, dev: Optional[int] = None,
+                         stream: int = 0):
+        dev = self.first_dev if dev is None else dev
+        self._check(self._lib.nttmul_pointwise_batch_device(self._h, _ptr(c), _ptr(a), _ptr(b),
+                                                            batch, word_bits, dev, stream or None))
 
     def multiply_device(self, c, a, b, batch: int, word_bits: int, dev: Optional[int] = None,
                         stream: int = 0):

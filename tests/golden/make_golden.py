@@ -77,6 +77,22 @@ def main():
                         b=B.astype(np.uint32),
                         **{k: v.astype(np.uint32) for k, v in outs.items()})
 
+    # 2b. standalone transforms at (256, 12289, psi = 1002) through the reference's own loops:
+    #     forward = mul_array16(psi_powers) + ntt_ct_std2rev(omega_powers_rev)  (ntt256.C:6-7)
+    #     inverse = ntt_gs_rev2std(inv_omega_powers_rev) + mul_array16(scaled_inv_psi) (:22-23)
+    P256 = O.Plan(256, Q0, 1002)
+    t = {k: P256.table(k).astype(np.uint16) for k in O.TABLES}
+    fwd = np.array([R.transform("ntt_ct_std2rev", R.transform("mul_array16", x, t["psi_powers"]),
+                                t["omega_powers_rev"]) for x in A])
+    fwd_gs = np.array([R.transform("ntt_gs_std2rev", R.transform("mul_array16", x, t["psi_powers"]),
+                                   t["omega_powers"]) for x in A])
+    assert np.array_equal(fwd, fwd_gs)
+    inv = np.array([R.transform("mul_array16", R.transform("ntt_gs_rev2std", x,
+                                                           t["inv_omega_powers_rev"]),
+                                t["scaled_inv_psi_powers"]) for x in A])
+    np.savez_compressed(os.path.join(HERE, "ref256_transforms.npz"), x=A.astype(np.uint32),
+                        forward=fwd.astype(np.uint32), inverse=inv.astype(np.uint32))
+
     # 3. n = 512, 1024, 2048 at q = 12289 through the reference's generic-n loops (ntt.C) fed with
     #    tables from the oracle planner (psi = smallest order-2n element, generate_params.C:25-44).
     gen = {}

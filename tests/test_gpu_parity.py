@@ -213,3 +213,55 @@ def test_multi_device_context_split(torch_cuda):
     P = O.Plan(2048, Q31)
     for i in range(9):
         assert np.array_equal(c[i], P.product_merged(a[i], b[i]))
+
+
+# ---------------------------------------------------------------------------------------------
+# Standalone transforms
+# ---------------------------------------------------------------------------------------------
+
+def test_transforms_ref256_golden(golden_dir, torch_cuda):
+    """forward == the reference's mul_array16(psi) + ntt_ct_std2rev (and the GS variant);
+    inverse == ntt_gs_rev2std + mul_array16(scaled_inv_psi), on the reference's own inputs."""
+    g = np.load(os.path.join(golden_dir, "ref256_transforms.npz"))
+    ctx = _ctx(256, Q0, psi=1002)
+    assert np.array_equal(ctx.forward(g["x"]), g["forward"])
+    assert np.array_equal(ctx.inverse(g["x"]), g["inverse"])
+
+
+@pytest.mark.parametrize("n", [256, 1024, 4096, 8192, 65536])
+@pytest.mark.parametrize("q", [Q31, Q62])
+def test_transforms_vs_oracle(n, q, torch_cuda):
+    P = O.Plan(n, q)
+    ctx = _ctx(n, q)
+    a, b = O.fill_inputs(n, q, 11, 3)
+    a[0] = q - 1
+    dt = np.uint32 if q < (1 << 32) else np.uint64
+    fa = ctx.forward(a.astype(dt)).astype(np.uint64)
+    fb = ctx.forward(b.astype(dt)).astype(np.uint64)
+    for i in range(3):
+        assert np.array_equal(fa[i], P.transform("mulntt_ct_std2rev", a[i], "mixed_powers_rev"))
+    assert np.array_equal(ctx.inverse(fa.astype(dt)).astype(np.uint64), a)      # round trip
+    pw = ctx.pointwise(fa.astype(dt), fb.astype(dt)).astype(np.uint64)
+    exp = np.array([[int(x) * int(y) % q for x, y in zip(r, s)] for r, s in zip(fa, fb)],
+                   dtype=np.uint64)
+    assert np.array_equal(pw, exp)
+    c = ctx.inverse(pw.astype(dt)).astype(np.uint64)                           # = a * b
+    assert np.array_equal(c, ctx.multiply(a.astype(dt), b.astype(dt)).astype(np.uint64))
+
+
+def test_transforms_device_path(torch_cuda):
+    torch = torch_cuda
+    n, q, batch = 4096, Q31, 4096
+    ctx = _ctx(n, q)
+    a = torch.empty(batch * n, dtype=torch.int32, device="cuda")
+    b = torch.empty_like(a)
+    s = torch.cuda.current_stream().cuda_stream
+    ctx.fill_random_device(a, b, 0, batch, 32, stream=s)
+    fa, fb, pw, c, c2 = (torch.empty_like(a) for _ in range(5))
+    ctx.forward_device(fa, a, batch, 32, stream=s)
+    ctx.forward_device(fb, b, batch, 32, stream=s)
+    ctx.pointwise_device(pw, fa, fb, batch, 32, stream=s)
+    ctx.inverse_device(c, pw, batch, 32, stream=s)
+    ctx.multiply_device(c2, a, b, batch, 32, stream=s)
+    torch.cuda.synchronize()
+    assert torch.equal(c, c2)
