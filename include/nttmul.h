@@ -46,6 +46,8 @@ extern "C" {
 #define NTTMUL_EUNSUPPORTED (-6) /* (n, q, word) combination outside the implemented kernels */
 
 #define NTTMUL_FLAG_VALIDATE 1u  /* range-check inputs on the device before multiplying */
+#define NTTMUL_FLAG_CYCLIC 2u    /* FPGA-compat: c = a*b mod (x^n - 1, q) (Hardware_Multiplier/
+                                    PolyMult.v); q == 1 (mod n); params.psi carries omega */
 
 typedef struct nttmul_ctx nttmul_ctx;
 
@@ -64,6 +66,7 @@ typedef struct {
   uint32_t word_bits;  /* 32: lazy 32-bit Shoup kernels (q < 2^31); 64: 64-bit kernels          */
   int ndev;
   int kernel;          /* 1 = fused single-launch polymult, 2 = multi-pass (n > 4096)             */
+  uint32_t cyclic;     /* 1 with NTTMUL_FLAG_CYCLIC (psi, inv_psi are 0 then)                    */
 } nttmul_info;
 
 /* ≙ PCIE_Load + PCIE_Open + mode-0 parameter/twiddle stream (NTT_PCIECommunicationv2.c:137-178) */
@@ -125,6 +128,46 @@ int nttmul_pointwise_batch_device(nttmul_ctx *ctx, void *c, const void *a, const
  * b[p][i] = splitmix64(seed + 2n(p0+p) + n + i) mod q, for p in [0, count).  Asynchronous. */
 int nttmul_fill_random_device(nttmul_ctx *ctx, void *a, void *b, uint64_t p0, size_t count,
                               uint64_t seed, int word_bits, int dev, void *stream);
+
+/* ---- Parameter / twiddle planner (host only, no device needed) ----------
+ * Replaces Generator_Params/ (generate_params.C:12-73, prime_generate.C:9-200, helper.C:5-35)
+ * and the precomputed NTT/ntt256_tables.C with run-time generation for any (n, q, psi). */
+int nttmul_is_prime(uint64_t q);                       /* deterministic Miller-Rabin, q < 2^64 */
+/* generate_params.C:25-44: the smallest element of multiplicative order exactly 2n (0: none) */
+uint64_t nttmul_smallest_psi(uint32_t n, uint64_t q);
+/* the smallest element of order exactly n (cyclic mode's omega; 0: none) */
+uint64_t nttmul_smallest_omega(uint32_t n, uint64_t q);
+/* Largest prime q < 2^bits with q == 1 (mod 2n) (mod n when cyclic), 3 <= bits <= 62: the
+ * deterministic counterpart of generate_params.C:16-20's random K-bit search.  0 / NTTMUL_EINVAL */
+int nttmul_find_prime(uint32_t n, int bits, int cyclic, uint64_t *q);
+/* The tables of NTT/ntt.h:63-183 for (n, q, psi), uint64 in [0, q), n entries; psi = 0 picks
+ * nttmul_smallest_psi.  which: 0 psi_powers, 1 inv_psi_powers, 2 inv_psi_powers_rev,
+ * 3 scaled_inv_psi_powers, 4 omega_powers, 5 omega_powers_rev, 6 inv_omega_powers,
+ * 7 inv_omega_powers_rev, 8 mixed_powers, 9 mixed_powers_rev, 10 inv_mixed_powers,
+ * 11 inv_mixed_powers_rev.  For n = 256, q = 12289, psi = 1002 these equal ntt256_tables.C. */
+int nttmul_table(uint32_t n, uint64_t q, uint64_t psi, int which, uint64_t *out);
+
+/* ---- FPGA-compat ----------------------------------------------------------
+ * R of generate_params.C:47-49: 2^((log2 n + 1) * ceil(K / (log2 n + 1))), K = bits of q */
+uint64_t nttmul_fpga_R(uint32_t n, int K);
+/* generate_twiddles (generate_params.C:54-73) / test_generator.py:184-189: the PolyMult.v twiddle
+ * stream W[idx] = w^((((P << j) k + (i << j)) mod n/2)) R mod q for j < log2 n,
+ * k < max(1, (n / 2P) >> j), i < P (P = PE_NUMBER, 8 on the DE2i-150).  Writes at most cap words,
+ * returns the stream length (272 for n = 256, P = 8).  Computed in 64-bit (no uint32 overflow). */
+size_t nttmul_fpga_twiddles(uint32_t n, uint64_t q, uint64_t w, uint64_t R, uint32_t P,
+                            uint64_t *out, size_t cap);
+
+/* ---- Text formats --------------------------------------------------------
+ * nttmul_read_coefficients: time_testing256.c:17-44 ler_coeficientes — up to max whitespace-
+ * separated decimal int32 values, stopping at EOF or the first invalid token; returns the count
+ * read, or -1 if the file cannot be opened.
+ * nttmul_read_hex: $readmemh files (test_generator.py:174-181 POLY_*_HEX.txt, NTT_DIN.txt): one
+ * hexadecimal word per line, '//' comments skipped; returns the count or -1.
+ * nttmul_print_array: time_testing256.c:46-64 print_array — 16 per row, "%5d", two-space indent. */
+int nttmul_read_coefficients(const char *path, int32_t *out, int max);
+int nttmul_read_hex(const char *path, uint64_t *out, int max);
+int nttmul_write_hex(const char *path, const uint64_t *a, int n);
+int nttmul_print_array(void *file /* FILE* */, const int32_t *a, int n);
 
 /* Compat shims with the reference's exact signatures and semantics: n = 256, q = 12289,
  * psi = 1002 (ntt256_tables.h:20-24), int32 coefficients in [0, q-1], result in c.  Like the

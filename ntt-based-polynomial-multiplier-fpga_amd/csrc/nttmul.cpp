@@ -204,7 +204,7 @@ int nttmul_create_ex(nttmul_ctx **out, const nttmul_params *prm) {
   *out = nullptr;
   nttmul_ctx *ctx = new (std::nothrow) nttmul_ctx();
   if (!ctx) return NTTMUL_ENOMEM;
-  int st = make_plan(prm->n, prm->q, prm->psi, &ctx->plan);
+  int st = make_plan(prm->n, prm->q, prm->psi, &ctx->plan, (prm->flags & NTTMUL_FLAG_CYCLIC) != 0);
   if (st) {
     delete ctx;
     return st;
@@ -285,6 +285,7 @@ int nttmul_get_info(const nttmul_ctx *ctx, nttmul_info *info) {
   info->word_bits = (uint32_t)P.word_bits;
   info->ndev = ctx->ndev;
   info->kernel = P.logn > 12 ? 2 : 1;
+  info->cyclic = P.cyclic ? 1 : 0;
   return NTTMUL_OK;
 }
 

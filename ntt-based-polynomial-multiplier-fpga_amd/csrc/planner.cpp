@@ -84,38 +84,79 @@ static void put_pairs(std::vector<uint8_t> &dst, const std::vector<uint64_t> &w,
   }
 }
 
-int make_plan(uint32_t n, uint64_t q, uint64_t psi, Plan *P) {
+uint64_t smallest_omega(uint32_t n, uint64_t q) {
+  if ((q - 1) % n) return 0;
+  uint64_t r = 0;
+  for (uint64_t g = 2; g < q && !r; g++) {
+    uint64_t c = powmod(g, (q - 1) / n, q);
+    if (powmod(c, n / 2, q) == q - 1) r = c;  // order exactly n
+  }
+  if (!r) return 0;
+  uint64_t best = r, cur = r;
+  for (uint64_t k = 2; k < n; k++) {          // primitive n-th roots: r^k, k odd
+    cur = mulmod(cur, r, q);
+    if ((k & 1) && cur < best) best = cur;
+  }
+  return best;
+}
+
+int make_plan(uint32_t n, uint64_t q, uint64_t psi, Plan *P, bool cyclic) {
   if (n < 256 || n > 65536 || (n & (n - 1))) return NTTMUL_EINVAL;
-  if (q < 3 || q >= (1ull << 62) || !is_prime(q) || (q - 1) % (2ull * n)) return NTTMUL_EINVAL;
-  if (!psi) psi = smallest_psi(n, q);
-  if (!psi || psi >= q || powmod(psi, n, q) != q - 1) return NTTMUL_EINVAL;
+  const uint64_t order = cyclic ? n : 2ull * n;
+  if (q < 3 || q >= (1ull << 62) || !is_prime(q) || (q - 1) % order) return NTTMUL_EINVAL;
+  if (cyclic) {
+    // FPGA-compat cyclic convolution (Hardware_Multiplier/PolyMult.v; test_generator/helper.py
+    // IterativeForwardNTT): `psi` carries the primitive n-th root omega, no psi weighting.
+    if (!psi) psi = smallest_omega(n, q);
+    if (!psi || psi >= q || powmod(psi, n / 2, q) != q - 1) return NTTMUL_EINVAL;
+  } else {
+    if (!psi) psi = smallest_psi(n, q);
+    if (!psi || psi >= q || powmod(psi, n, q) != q - 1) return NTTMUL_EINVAL;
+  }
+  P->cyclic = cyclic;
   P->n = n;
   P->logn = 0;
   while ((1u << P->logn) < n) P->logn++;
   P->q = q;
-  P->psi = psi;
-  P->omega = mulmod(psi, psi, q);
-  P->inv_psi = powmod(psi, q - 2, q);
-  P->inv_omega = mulmod(P->inv_psi, P->inv_psi, q);
+  P->psi = cyclic ? 0 : psi;
+  P->omega = cyclic ? psi : mulmod(psi, psi, q);
+  P->inv_psi = cyclic ? 0 : powmod(psi, q - 2, q);
+  P->inv_omega = powmod(P->omega, q - 2, q);
   P->inv_n = powmod(n, q - 2, q);
   P->word_bits = q < (1ull << 31) ? 32 : 64;
   const int bits = P->word_bits;
 
-  // psi^k, k in [0, 2n): every twiddle is a power of psi (psi^(2n) = 1)
-  const uint32_t two_n = 2 * n;
-  std::vector<uint64_t> pw(two_n);
-  pw[0] = 1;
-  for (uint32_t k = 1; k < two_n; k++) pw[k] = mulmod(pw[k - 1], psi, q);
-  // mixed_powers_rev[t+j] = psi^(n/2t) omega^((n/2t) bitrev(j)) = psi^(e (1 + 2 bitrev(j))),
-  // inv_mixed_powers_rev = its inverse (ntt.h:120-127, :145-155; ntt256.h:58,63)
   std::vector<uint64_t> fw(n, 0), iw(n, 0);
   uint32_t lt = 0;
-  for (uint32_t t = 1; t < n; t <<= 1, lt++) {
-    const uint64_t e = n / (2ull * t);
-    for (uint32_t j = 0; j < t; j++) {
-      const uint64_t ex = (e * (1 + 2ull * bitrev(j, lt))) % two_n;
-      fw[t + j] = pw[ex];
-      iw[t + j] = pw[(two_n - ex) % two_n];
+  if (!cyclic) {
+    // psi^k, k in [0, 2n): every twiddle is a power of psi (psi^(2n) = 1)
+    const uint32_t two_n = 2 * n;
+    std::vector<uint64_t> pw(two_n);
+    pw[0] = 1;
+    for (uint32_t k = 1; k < two_n; k++) pw[k] = mulmod(pw[k - 1], psi, q);
+    // mixed_powers_rev[t+j] = psi^(n/2t) omega^((n/2t) bitrev(j)) = psi^(e (1 + 2 bitrev(j))),
+    // inv_mixed_powers_rev = its inverse (ntt.h:120-127, :145-155; ntt256.h:58,63)
+    for (uint32_t t = 1; t < n; t <<= 1, lt++) {
+      const uint64_t e = n / (2ull * t);
+      for (uint32_t j = 0; j < t; j++) {
+        const uint64_t ex = (e * (1 + 2ull * bitrev(j, lt))) % two_n;
+        fw[t + j] = pw[ex];
+        iw[t + j] = pw[(two_n - ex) % two_n];
+      }
+    }
+  } else {
+    // omega_powers_rev[t+j] = omega^((n/2t) bitrev(j)) and inv_omega_powers_rev (ntt.h:110-117,
+    // :134-143): the reference's plain ntt_ct_std2rev / ntt_gs_rev2std tables (ntt256.h:37,49)
+    std::vector<uint64_t> pw(n);
+    pw[0] = 1;
+    for (uint32_t k = 1; k < n; k++) pw[k] = mulmod(pw[k - 1], P->omega, q);
+    for (uint32_t t = 1; t < n; t <<= 1, lt++) {
+      const uint64_t e = n / (2ull * t);
+      for (uint32_t j = 0; j < t; j++) {
+        const uint64_t ex = (e * bitrev(j, lt)) % n;
+        fw[t + j] = pw[ex];
+        iw[t + j] = pw[(n - ex) % n];
+      }
     }
   }
   if (bits == 32) {

@@ -18,8 +18,11 @@ uint64_t powmod(uint64_t b, uint64_t e, uint64_t q);
 bool is_prime(uint64_t n);
 // generate_params.C:25-44 rule: the smallest integer of multiplicative order exactly 2n.
 uint64_t smallest_psi(uint32_t n, uint64_t q);
+// the smallest integer of multiplicative order exactly n (cyclic / FPGA-compat mode)
+uint64_t smallest_omega(uint32_t n, uint64_t q);
 
 struct Plan {
+  bool cyclic = false;               // x^n - 1 (FPGA-compat) instead of x^n + 1
   uint32_t n = 0, logn = 0;
   uint64_t q = 0, psi = 0, omega = 0, inv_psi = 0, inv_omega = 0, inv_n = 0;
   int word_bits = 0;                 // 32 when q < 2^31 (lazy [0, 2q) fits a u32), else 64
@@ -30,6 +33,6 @@ struct Plan {
 };
 
 // Returns 0 or a negative NTTMUL_E* status.
-int make_plan(uint32_t n, uint64_t q, uint64_t psi, Plan *out);
+int make_plan(uint32_t n, uint64_t q, uint64_t psi, Plan *out, bool cyclic = false);
 
 }  // namespace nttmul

@@ -27,6 +27,12 @@ NTTMUL_ENOMEM = -4
 NTTMUL_ERANGE = -5
 NTTMUL_EUNSUPPORTED = -6
 NTTMUL_FLAG_VALIDATE = 1
+NTTMUL_FLAG_CYCLIC = 2
+TABLES = [  # nttmul_table `which` order = the tables of NTT/ntt.h:63-183 (ntt256_tables.h:29-43)
+    "psi_powers", "inv_psi_powers", "inv_psi_powers_rev", "scaled_inv_psi_powers",
+    "omega_powers", "omega_powers_rev", "inv_omega_powers", "inv_omega_powers_rev",
+    "mixed_powers", "mixed_powers_rev", "inv_mixed_powers", "inv_mixed_powers_rev",
+]
 
 SEED = 0x4E54544D554C  # "NTTMUL", SURVEY §8d
 
@@ -47,7 +53,7 @@ class Info(ctypes.Structure):
                 ("psi", ctypes.c_uint64), ("omega", ctypes.c_uint64),
                 ("inv_psi", ctypes.c_uint64), ("inv_omega", ctypes.c_uint64),
                 ("inv_n", ctypes.c_uint64), ("word_bits", ctypes.c_uint32),
-                ("ndev", ctypes.c_int), ("kernel", ctypes.c_int)]
+                ("ndev", ctypes.c_int), ("kernel", ctypes.c_int), ("cyclic", ctypes.c_uint32)]
 
 
 _LIB: Optional[ctypes.CDLL] = None
@@ -84,6 +90,21 @@ def load_library() -> ctypes.CDLL:
         getattr(lib, f"nttmul_pointwise_batch_{w}").argtypes = [vp, vp, vp, vp, sz]
     lib.nttmul_pointwise_batch_device.argtypes = [vp, vp, vp, vp, sz, i32, i32, vp]
     lib.nttmul_fill_random_device.argtypes = [vp, vp, vp, u64, sz, u64, i32, i32, vp]
+    lib.nttmul_is_prime.argtypes = [u64]
+    lib.nttmul_smallest_psi.argtypes = [u32, u64]
+    lib.nttmul_smallest_psi.restype = u64
+    lib.nttmul_smallest_omega.argtypes = [u32, u64]
+    lib.nttmul_smallest_omega.restype = u64
+    lib.nttmul_find_prime.argtypes = [u32, i32, i32, ctypes.POINTER(u64)]
+    lib.nttmul_table.argtypes = [u32, u64, u64, i32, vp]
+    lib.nttmul_fpga_R.argtypes = [u32, i32]
+    lib.nttmul_fpga_R.restype = u64
+    lib.nttmul_fpga_twiddles.argtypes = [u32, u64, u64, u64, u32, vp, sz]
+    lib.nttmul_fpga_twiddles.restype = sz
+    lib.nttmul_read_coefficients.argtypes = [ctypes.c_char_p, vp, i32]
+    lib.nttmul_read_hex.argtypes = [ctypes.c_char_p, vp, i32]
+    lib.nttmul_write_hex.argtypes = [ctypes.c_char_p, vp, i32]
+    lib.nttmul_print_array.argtypes = [vp, vp, i32]
     for name in ("ntt256_product1", "ntt256_product4", "ntt_red256_product1", "ntt_red256_product4"):
         getattr(lib, name).argtypes = [vp, vp, vp]
         getattr(lib, name).restype = None
@@ -118,10 +139,13 @@ class Context:
     """An (n, q) multiplier bound to one or more HIP devices (≙ an opened FPGA handle)."""
 
     def __init__(self, n: int, q: int, psi: int = 0, ndev: int = 1, first_dev: int = 0,
-                 validate: bool = False):
+                 validate: bool = False, cyclic: bool = False):
+        """cyclic=True: FPGA-compat product mod (x^n - 1, q) (Hardware_Multiplier/PolyMult.v);
+        `psi` then carries the primitive n-th root omega (0 = the smallest one)."""
         self._lib = load_library()
         self._h = ctypes.c_void_p()
-        prm = _Params(n, q, psi, ndev, first_dev, NTTMUL_FLAG_VALIDATE if validate else 0)
+        flags = (NTTMUL_FLAG_VALIDATE if validate else 0) | (NTTMUL_FLAG_CYCLIC if cyclic else 0)
+        prm = _Params(n, q, psi, ndev, first_dev, flags)
         st = self._lib.nttmul_create_ex(ctypes.byref(self._h), ctypes.byref(prm))
         if st != NTTMUL_OK:
             raise NttmulError(st, strerror(st))
@@ -230,6 +254,77 @@ class Context:
         dev = self.first_dev if dev is None else dev
         self._check(self._lib.nttmul_fill_random_device(self._h, _ptr(a), _ptr(b), p0, count, seed,
                                                         word_bits, dev, stream or None))
+
+
+# ---- planner API ------------------------------------------------------------
+
+def is_prime(q: int) -> bool:
+    return bool(load_library().nttmul_is_prime(q))
+
+
+def smallest_psi(n: int, q: int) -> int:
+    """generate_params.C:25-44: smallest element of order exactly 2n (0 if none)."""
+    return int(load_library().nttmul_smallest_psi(n, q))
+
+
+def smallest_omega(n: int, q: int) -> int:
+    return int(load_library().nttmul_smallest_omega(n, q))
+
+
+def find_prime(n: int, bits: int, cyclic: bool = False) -> int:
+    """Largest prime q < 2^bits with q == 1 (mod 2n) (mod n if cyclic)."""
+    q = ctypes.c_uint64()
+    st = load_library().nttmul_find_prime(n, bits, int(cyclic), ctypes.byref(q))
+    if st != NTTMUL_OK:
+        raise NttmulError(st, strerror(st))
+    return q.value
+
+
+def table(n: int, q: int, name: str, psi: int = 0) -> np.ndarray:
+    """One of the NTT/ntt.h:63-183 tables for (n, q, psi)."""
+    out = np.zeros(n, dtype=np.uint64)
+    st = load_library().nttmul_table(n, q, psi, TABLES.index(name), out.ctypes.data)
+    if st != NTTMUL_OK:
+        raise NttmulError(st, strerror(st))
+    return out
+
+
+def fpga_R(n: int, K: int) -> int:
+    return int(load_library().nttmul_fpga_R(n, K))
+
+
+def fpga_twiddles(n: int, q: int, w: int, R: int, P: int = 8) -> np.ndarray:
+    """generate_twiddles (generate_params.C:54-73): the PolyMult.v W / W_INV stream."""
+    lib = load_library()
+    cnt = lib.nttmul_fpga_twiddles(n, q, w, R, P, None, 0)
+    out = np.zeros(cnt, dtype=np.uint64)
+    lib.nttmul_fpga_twiddles(n, q, w, R, P, out.ctypes.data, cnt)
+    return out
+
+
+# ---- text formats (SURVEY §8f row 4) ------------------------------------------------------------
+
+def read_coefficients(path: str, max_count: int) -> np.ndarray:
+    """time_testing256.c:17-44 ler_coeficientes."""
+    out = np.zeros(max_count, dtype=np.int32)
+    cnt = load_library().nttmul_read_coefficients(path.encode(), out.ctypes.data, max_count)
+    if cnt < 0:
+        raise OSError(f"cannot open {path}")
+    return out[:cnt]
+
+
+def read_hex(path: str, max_count: int) -> np.ndarray:
+    out = np.zeros(max_count, dtype=np.uint64)
+    cnt = load_library().nttmul_read_hex(path.encode(), out.ctypes.data, max_count)
+    if cnt < 0:
+        raise OSError(f"cannot open {path}")
+    return out[:cnt]
+
+
+def write_hex(path: str, a) -> None:
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    if load_library().nttmul_write_hex(path.encode(), a.ctypes.data, a.size) < 0:
+        raise OSError(f"cannot write {path}")
 
 
 def multiply(a, b, n: int, q: int) -> np.ndarray:

@@ -449,6 +449,21 @@ void orc_schoolbook(uint64_t *c, const uint64_t *a, const uint64_t *b, uint32_t 
   }
 }
 
+/* Cyclic counterpart, c = a*b mod (x^n - 1, q): what Hardware_Multiplier/PolyMult.v computes
+ * (test_generator/helper.py IterativeForwardNTT/IterativeInverseNTT flow, no psi). */
+void orc_cyclic_schoolbook(uint64_t *c, const uint64_t *a, const uint64_t *b, uint32_t n,
+                           uint64_t q) {
+  for (uint32_t k = 0; k < n; k++) c[k] = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    uint64_t ai = a[i] % q;
+    if (!ai) continue;
+    for (uint32_t j = 0; j < n; j++) {
+      uint32_t k = (i + j) & (n - 1);
+      c[k] = add_mod(c[k], mulmod(ai, b[j] % q, q), q);
+    }
+  }
+}
+
 /* Evaluation check: r = psi^(2k+1) is a root of x^n + 1, so
  * c(r) == a(r) b(r) (mod q).  Returns the number of failing points among nk. */
 int orc_eval_check(const orc_plan *P, const uint64_t *c, const uint64_t *a, const uint64_t *b,

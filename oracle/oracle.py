@@ -64,6 +64,7 @@ def _load() -> ctypes.CDLL:
     lib.orc_scalar_mul_array.argtypes = [_u64p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64]
     lib.orc_bitrev_shuffle.argtypes = [_u64p, ctypes.c_uint32]
     lib.orc_schoolbook.argtypes = [_u64p, _u64p, _u64p, ctypes.c_uint32, ctypes.c_uint64]
+    lib.orc_cyclic_schoolbook.argtypes = [_u64p, _u64p, _u64p, ctypes.c_uint32, ctypes.c_uint64]
     lib.orc_eval_check.restype = ctypes.c_int
     lib.orc_eval_check.argtypes = [ctypes.c_void_p, _u64p, _u64p, _u64p, ctypes.c_uint32]
     lib.orc_red_product.restype = ctypes.c_int
@@ -207,6 +208,15 @@ def schoolbook(a, b, n: int, q: int) -> np.ndarray:
     b = np.array(b, dtype=np.uint64, copy=True)
     c = np.zeros(n, dtype=np.uint64)
     lib().orc_schoolbook(_p64(c), _p64(a), _p64(b), n, q)
+    return c
+
+
+def cyclic_schoolbook(a, b, n: int, q: int) -> np.ndarray:
+    """c = a*b mod (x^n - 1, q): the FPGA's cyclic product (Hardware_Multiplier/PolyMult.v)."""
+    a = np.array(a, dtype=np.uint64, copy=True)
+    b = np.array(b, dtype=np.uint64, copy=True)
+    c = np.zeros(n, dtype=np.uint64)
+    lib().orc_cyclic_schoolbook(_p64(c), _p64(a), _p64(b), n, q)
     return c
 
 

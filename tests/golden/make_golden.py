@@ -107,6 +107,37 @@ def main():
         gen[f"n{n}_c"] = c1.astype(np.uint32); gen[f"n{n}_psi"] = np.array([P.psi])
     np.savez_compressed(os.path.join(HERE, "ref_generic_12289.npz"), **gen)
 
+    # 2c. cyclic transforms through the reference's plain (non-psi) loops, ntt256.h:37,49:
+    #     ntt_ct_std2rev(omega_powers_rev) and ntt_gs_rev2std(inv_omega_powers_rev) + n^-1
+    cfw = np.array([R.transform("ntt_ct_std2rev", x, t["omega_powers_rev"]) for x in A])
+    cinv = np.array([R.scalar_mul_array(R.transform("ntt_gs_rev2std", x, t["inv_omega_powers_rev"]),
+                                        P256.inv_n) for x in A])
+    np.savez_compressed(os.path.join(HERE, "ref256_cyclic.npz"), x=A.astype(np.uint32),
+                        omega=np.array([P256.omega]), forward=cfw.astype(np.uint32),
+                        inverse=cinv.astype(np.uint32))
+
+    # 2d. the FPGA's own committed simulation vectors (Hardware_Multiplier/simulation/modelsim/
+    #     test/*.txt, data files of the reference) + the cyclic product of its POLY_A x POLY_B
+    hm = "/root/reference/Multiplier_NTT_Based/Hardware_Multiplier/simulation/modelsim/test"
+    def rd(name):
+        vals = []
+        for line in open(os.path.join(hm, name)):
+            line = line.strip()
+            if line and not line.startswith("//"):
+                vals.append(int(line.split()[0], 16))
+        return np.array(vals, dtype=np.uint64)
+    prm = rd("PARAM.txt")  # N, q, w, w_inv, psi, psi_inv, n_inv*R, R
+    fv = {k: rd(k.upper() + ".txt") for k in ("ntt_din", "ntt_dout", "intt_din", "intt_dout",
+                                                  "w", "winv", "poly_a_hex", "poly_b_hex")}
+    n_f, q_f = int(prm[0]), int(prm[1])
+    fv["poly_c_cyclic"] = O.cyclic_schoolbook(fv["poly_a_hex"], fv["poly_b_hex"], n_f, q_f)
+    np.savez_compressed(os.path.join(HERE, "fpga_vectors.npz"), param=prm, **fv)
+    # text fixtures for the reference's file formats (copies of its data files)
+    import shutil
+    for name in ("coeficientes_a.txt", "coeficientes_b.txt"):
+        shutil.copy(os.path.join(REF_DIR, name), os.path.join(HERE, name))
+    shutil.copy(os.path.join(hm, "POLY_A_HEX.txt"), os.path.join(HERE, "POLY_A_HEX.txt"))
+
     # 4. BASELINE moduli the reference cannot run: big-int schoolbook (schoolbook.py:23-46).
     sb = {}
     cases = [(1024, 2013265921, 3), (4096, 2013265921, 2), (1024, 4293918721, 2),

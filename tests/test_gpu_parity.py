@@ -265,3 +265,56 @@ def test_transforms_device_path(torch_cuda):
     ctx.multiply_device(c2, a, b, batch, 32, stream=s)
     torch.cuda.synchronize()
     assert torch.equal(c, c2)
+
+
+# ---------------------------------------------------------------------------------------------
+# FPGA-compat cyclic mode and the reference's timing harness (row 4)
+# ---------------------------------------------------------------------------------------------
+
+def test_cyclic_reference_loops(golden_dir, torch_cuda):
+    """Cyclic mode's transforms are the reference's plain ntt256_ct_std2rev / gs_rev2std (+ n^-1)."""
+    g = np.load(os.path.join(golden_dir, "ref256_cyclic.npz"))
+    ctx = _ctx(256, Q0, psi=int(g["omega"][0]), cyclic=True)
+    assert ctx.info.cyclic == 1
+    assert np.array_equal(ctx.forward(g["x"]), g["forward"])
+    assert np.array_equal(ctx.inverse(g["x"]), g["inverse"])
+
+
+def test_cyclic_fpga_vectors(golden_dir, torch_cuda):
+    """The FPGA's committed ModelSim vectors (q = 7681, w = 3844): NTT_DIN -> NTT_DOUT, the
+    inverse back, and the cyclic product of POLY_A x POLY_B (Hardware_Multiplier/PolyMult.v)."""
+    g = np.load(os.path.join(golden_dir, "fpga_vectors.npz"))
+    n, q, w = (int(v) for v in g["param"][:3])
+    ctx = _ctx(n, q, psi=w, cyclic=True)
+    assert np.array_equal(ctx.forward(g["ntt_din"]).astype(np.uint64), g["ntt_dout"])
+    assert np.array_equal(ctx.inverse(g["ntt_dout"]).astype(np.uint64), g["ntt_din"])
+    c = ctx.multiply(g["poly_a_hex"], g["poly_b_hex"]).astype(np.uint64)
+    assert np.array_equal(c, g["poly_c_cyclic"])
+    a = np.zeros(n, np.uint32); a[:3] = [1, 2, 3]                # NTT_PolyMul_test.v:110-195 KAT
+    b = np.zeros(n, np.uint32); b[:2] = [2, 2]
+    assert list(ctx.multiply(a, b)[:5]) == [2, 6, 10, 6, 0]
+
+
+@pytest.mark.parametrize("n,q", [(1024, Q31), (4096, Q31), (8192, Q31), (2048, Q62)])
+def test_cyclic_vs_schoolbook(n, q, torch_cuda):
+    ctx = _ctx(n, q, cyclic=True)
+    a, b = O.fill_inputs(n, q, 3, 2)
+    a[1] = q - 1
+    dt = np.uint32 if q < (1 << 32) else np.uint64
+    c = ctx.multiply(a.astype(dt), b.astype(dt)).astype(np.uint64)
+    for i in range(2):
+        assert np.array_equal(c[i], O.cyclic_schoolbook(a[i], b[i], n, q)), (n, q, i)
+
+
+def test_time_testing_gpu_app(golden_dir, torch_cuda):
+    """apps/time_testing_gpu (time_testing256.c on the C ABI) prints the reference's product of
+    the reference's own coefficient files."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(nttmul.LIB_PATH), "..", "apps", "time_testing_gpu")
+    out = subprocess.run([exe, os.path.join(golden_dir, "coeficientes_a.txt"),
+                          os.path.join(golden_dir, "coeficientes_b.txt"), "5", "1024"],
+                         capture_output=True, text=True, timeout=120, check=True).stdout
+    g = np.load(os.path.join(golden_dir, "ref256.npz"))
+    vals = [int(x) for line in out.split("Resultado C = A * B):")[1].split("\n") for x in line.split()]
+    assert vals == [int(v) for v in g["ntt256_product4"][0]]
+    assert "Batch 1024" in out
