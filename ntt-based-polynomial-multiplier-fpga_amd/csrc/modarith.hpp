@@ -90,6 +90,14 @@ struct Arith32 {
   __device__ __forceinline__ uint32_t canon(uint32_t x) const { return csub(x, q); }
 };
 
+// 64-bit arithmetic on a 32-bit VALU.  q < 2^62 leaves two bits of headroom, so butterflies use
+// Harvey's lazy bounds (values in [0, 4q), one conditional subtraction per butterfly instead of
+// two), and the Shoup high product is spelled out in 32-bit limbs so hipcc emits v_mad_u64_u32 /
+// v_mul_hi_u32 / v_mul_lo_u32 directly (tools/kbench A/B: NTTMUL_A64_PLAIN=1 restores the
+// generic __umul64hi / [0, 2q) form).
+#ifndef NTTMUL_A64_PLAIN
+#define NTTMUL_A64_PLAIN 0
+#endif
 struct Arith64 {
   using word = uint64_t;
   static constexpr int kBits = 64;
@@ -100,10 +108,37 @@ struct Arith64 {
     uint64_t d;
     return __builtin_sub_overflow(x, m, &d) ? x : d;
   }
-  __device__ __forceinline__ uint64_t shoup(uint64_t x, uint64_t w, uint64_t ws) const {
-    uint64_t qh = __umul64hi(x, ws);
-    return x * w - qh * q;
+  // high 64 bits of the 128-bit product x * s, from four 32x32 products
+  __device__ __forceinline__ static uint64_t mulhi64(uint64_t x, uint64_t s) {
+#if NTTMUL_A64_PLAIN
+    return __umul64hi(x, s);
+#else
+    const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
+    const uint32_t sl = (uint32_t)s, sh = (uint32_t)(s >> 32);
+    const uint64_t t = (uint64_t)xl * sh + __umulhi(xl, sl);
+    const uint64_t u = (uint64_t)xh * sl + (uint32_t)t;
+    return (uint64_t)xh * sh + ((t >> 32) + (u >> 32));
+#endif
   }
+  // low 64 bits of x * w
+  __device__ __forceinline__ static uint64_t mullo64(uint64_t x, uint64_t w) {
+#if NTTMUL_A64_PLAIN
+    return x * w;
+#else
+    const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
+    const uint32_t wl = (uint32_t)w, wh = (uint32_t)(w >> 32);
+    const uint64_t a = (uint64_t)xl * wl;
+    const uint32_t hi = (uint32_t)(a >> 32) + xl * wh + xh * wl;
+    return ((uint64_t)hi << 32) | (uint32_t)a;
+#endif
+  }
+  // x * w mod q in [0, 2q) for any 64-bit x (Shoup, w' = floor(w 2^64 / q))
+  __device__ __forceinline__ uint64_t shoup(uint64_t x, uint64_t w, uint64_t ws) const {
+    const uint64_t qh = mulhi64(x, ws);
+    return mullo64(x, w) - mullo64(qh, q);
+  }
+#if NTTMUL_A64_PLAIN
+  static constexpr uint64_t kLazy = 2;  // values in [0, 2q)
   __device__ __forceinline__ void ct(uint64_t &X, uint64_t &Y, uint64_t w, uint64_t ws) const {
     uint64_t x = csub(X, q);
     uint64_t t = csub(shoup(Y, w, ws), q);
@@ -121,17 +156,41 @@ struct Arith64 {
     X = shoup(x + y, f, fs);
     Y = shoup(x - y + q, wf, wfs);
   }
-  // Montgomery a b 2^-64 mod q; a, b in [0, 2q) -> [0, 2q).  q < 2^62.
+  __device__ __forceinline__ uint64_t canon(uint64_t x) const { return csub(x, q); }
+#else
+  static constexpr uint64_t kLazy = 4;  // forward values in [0, 4q), inverse values in [0, 2q)
+  // Harvey CT: X in [0, 4q), any Y -> outputs in [0, 4q)
+  __device__ __forceinline__ void ct(uint64_t &X, uint64_t &Y, uint64_t w, uint64_t ws) const {
+    const uint64_t x = csub(X, 2 * q);
+    const uint64_t t = shoup(Y, w, ws);
+    X = x + t;
+    Y = x - t + 2 * q;
+  }
+  // Harvey GS: X, Y in [0, 2q) -> outputs in [0, 2q)
+  __device__ __forceinline__ void gs(uint64_t &X, uint64_t &Y, uint64_t w, uint64_t ws) const {
+    const uint64_t x = X, y = Y;
+    X = csub(x + y, 2 * q);
+    Y = shoup(x - y + 2 * q, w, ws);
+  }
+  __device__ __forceinline__ void gs_scaled(uint64_t &X, uint64_t &Y, uint64_t f, uint64_t fs,
+                                            uint64_t wf, uint64_t wfs) const {
+    const uint64_t x = X, y = Y;
+    X = shoup(x + y, f, fs);
+    Y = shoup(x - y + 2 * q, wf, wfs);
+  }
+  // [0, 4q) -> [0, q)
+  __device__ __forceinline__ uint64_t canon(uint64_t x) const { return csub(csub(x, 2 * q), q); }
+#endif
+  // Montgomery a b 2^-64 mod q; a, b lazy (< kLazy q) -> [0, 2q).  q < 2^62.
   __device__ __forceinline__ uint64_t mont(uint64_t a, uint64_t b) const {
-    a = csub(a, q);
-    b = csub(b, q);
-    uint64_t lo = a * b, hi = __umul64hi(a, b);
-    uint64_t m = lo * qinv_neg;
-    uint64_t mlo = m * q, mhi = __umul64hi(m, q);
-    uint64_t s = lo + mlo;
+    a = canon(a);
+    b = canon(b);
+    const uint64_t lo = mullo64(a, b), hi = mulhi64(a, b);
+    const uint64_t m = mullo64(lo, qinv_neg);
+    const uint64_t mlo = mullo64(m, q), mhi = mulhi64(m, q);
+    const uint64_t s = lo + mlo;
     return hi + mhi + (s < lo ? 1 : 0);  // (t + m q) / 2^64 < 2q
   }
-  __device__ __forceinline__ uint64_t canon(uint64_t x) const { return csub(x, q); }
 };
 
 // Twiddle + Shoup companion, stored interleaved so one load fetches both.
