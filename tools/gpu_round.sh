@@ -11,6 +11,6 @@ tail -2 $OUT/gpu_tests.log
 timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err
 cat $OUT/bench.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d $OUT/trace -o trace --output-format csv -- \
-  python3 bench.py --no-cpu-baseline --steps 10 --warmup 2 > $OUT/trace.log 2>&1
+  python3 bench.py --no-cpu-baseline --steps 200 --warmup 20 > $OUT/trace.log 2>&1
 timeout -k 10 600 tools/profile_pmc.sh $OUT/pmc > $OUT/pmc.log 2>&1
 echo "done $TAG"
