@@ -70,6 +70,8 @@ def parse(argv=None):
     ap.add_argument("--batch-per-gpu", type=int, default=65536)
     ap.add_argument("--word-bits", type=int, default=0, help="32/64 coefficient storage (0: auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--host-io", action="store_true",
+                    help="also time the host-buffer ABI path (PCIe-inclusive; never the value)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target wall time of the CPU-baseline sample")
     return ap.parse_args(argv)
@@ -99,6 +101,26 @@ def cpu_baseline(n: int, q: int, target_s: float):
             "sample": f"{per * reps} polymults (n={n}, q={q}) = {reps} passes over {per} "
                       f"counter-based inputs, OpenMP {threads} threads, "
                       f"{total_t:.1f} s, oracle/nttmul_oracle.c orc_fast_batch_u32"}
+
+
+def host_io(ctx, a_dev, b_dev, batch: int, n: int, wb: int, reps: int = 3):
+    """PCIe-inclusive rate of the host-buffer ABI path (nttmul_multiply_batch_u*: H2D a, b ->
+    product -> D2H c, the FPGA transaction of NTT_PCIECommunicationv2.c:164-229), same inputs."""
+    import numpy as np
+    dt = np.uint32 if wb == 32 else np.uint64
+    a = a_dev.cpu().numpy().view(dt).reshape(batch, n)
+    b = b_dev.cpu().numpy().view(dt).reshape(batch, n)
+    ctx.multiply(a[:1], b[:1])                           # staging buffers allocated once
+    best = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        ctx.multiply(a, b)
+        t = time.perf_counter() - t0
+        best = t if best is None else min(best, t)
+    return {"value": batch / best, "unit": "polymults/s", "seconds": best,
+            "bytes_over_pcie": 3 * n * (wb // 8) * batch,
+            "note": "host numpy buffers through nttmul_multiply_batch (PCIe-inclusive), best of "
+                    f"{reps}; reported beside, never the bench value"}
 
 
 def load_traffic(n: int, q: int, batch: int):
@@ -198,6 +220,8 @@ def main(argv=None):
                          "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": None,
         }
+        if args.host_io:
+            line["host_io"] = host_io(ctx, a, b, p1 - p0, n, wb)
         if world == 1 and not args.no_cpu_baseline:
             try:
                 line["cpu_baseline"] = cpu_baseline(n, q, args.cpu_seconds)

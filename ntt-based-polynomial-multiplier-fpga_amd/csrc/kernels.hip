@@ -28,6 +28,14 @@
 #ifndef NTTMUL_LDS_REGIONS
 #define NTTMUL_LDS_REGIONS 2
 #endif
+// skip the reduction of X in the first forward stage (input canonical by contract)
+#ifndef NTTMUL_FIRST_XC
+#define NTTMUL_FIRST_XC 1
+#endif
+// twiddle-traffic ablation (tools/kbench only; results are wrong when set): index & mask
+#ifndef NTTMUL_ABL_TWMASK
+#define NTTMUL_ABL_TWMASK 0
+#endif
 // __launch_bounds__ minimum waves per SIMD for k_rows (1 = no constraint)
 #ifndef NTTMUL_MIN_WAVES
 #define NTTMUL_MIN_WAVES 1
@@ -119,9 +127,16 @@ __device__ __forceinline__ void fwd_group(const A &ar, typename A::word (&x)[16]
       if (k & dist) continue;
       const int m = k / ns;
       const int idx = tbase + (Gr::blk(g, j, k) << l) + (m >> (S - l));
-      const TwPair<typename A::word> t = tw[idx];
-      ar.ct(x[k], x[k + dist], t.w, t.ws);
-      if (NPOLY == 2) ar.ct(y[k], y[k + dist], t.w, t.ws);
+      const TwPair<typename A::word> t = tw[NTTMUL_ABL_TWMASK ? (idx & NTTMUL_ABL_TWMASK) : idx];
+      // global stage 0 of a whole polynomial reads canonical input (the API contract, [0, q)):
+      // its X operands need no reduction
+      if (NTTMUL_FIRST_XC && g == 0 && l == 0 && l1 == 0) {
+        ar.template ct<true>(x[k], x[k + dist], t.w, t.ws);
+        if (NPOLY == 2) ar.template ct<true>(y[k], y[k + dist], t.w, t.ws);
+      } else {
+        ar.ct(x[k], x[k + dist], t.w, t.ws);
+        if (NPOLY == 2) ar.ct(y[k], y[k + dist], t.w, t.ws);
+      }
     }
   }
 }
@@ -146,7 +161,7 @@ __device__ __forceinline__ void inv_group(const KParams<A> &P, typename A::word 
       } else {
         const int m = k / ns;
         const int idx = tbase + (Gr::blk(g, j, k) << l) + (m >> (S - l));
-        const TwPair<typename A::word> t = tw[idx];
+        const TwPair<typename A::word> t = tw[NTTMUL_ABL_TWMASK ? (idx & NTTMUL_ABL_TWMASK) : idx];
         P.ar.gs(x[k], x[k + dist], t.w, t.ws);
       }
     }

@@ -11,10 +11,11 @@ struct LaunchTables {
   uint32_t logn;
   int word_bits;           // 32 -> Arith32 (q < 2^31), 64 -> Arith64
   uint64_t q, qinv_neg;    // -q^-1 mod 2^word_bits
-  uint64_t f, fs, wf, wfs; // F = n^-1 R mod q and iw[1] F, with Shoup companions
+  uint64_t f, fs, wf, wfs; // F = n^-1 R mod q and iw[1] F, as (value, companion) pairs
   uint64_t fi, fis, wfi, wfis; // n^-1 and iw[1] n^-1 (standalone inverse), with companions
   uint64_t r2;             // R^2 mod q (standalone pointwise product)
-  const void *fw, *iw;     // forward / inverse twiddle pairs {w, floor(w R / q)}, n entries
+  const void *fw, *iw;     // forward / inverse twiddle (value, companion) pairs, n entries
+                           // (planner.cpp tw_pair: Shoup, or Montgomery form for Arith32)
   int cus;                 // compute units of the device (persistent grid size)
 };
 

@@ -4,7 +4,8 @@
 // divq/modq; NTT-RED/ntt_red.c:34-46 K-RED) with word-size-generic lazy Shoup butterflies:
 //
 //   Arith32 : q < 2^31, values kept in [0, 2q) inside 32-bit registers.  A twiddle product is
-//             one v_mul_hi_u32 + two v_mul_lo_u32 (Shoup, w' = floor(w 2^32 / q)); a conditional
+//             one v_mul_lo_u32 + two v_mad_u64_u32 with the twiddle in Montgomery form (or,
+//             NTTMUL_A32_MONT=0, Shoup: v_mul_hi_u32 + two v_mul_lo_u32 + v_sub); a conditional
 //             subtraction is v_sub_co_u32 + v_cndmask_b32 (no compare/branch).
 //   Arith64 : q < 2^62, values in [0, 2q) in 64-bit registers, 64x64 Shoup via __umul64hi.
 //             Also used for 32-bit words with 2^31 <= q < 2^32 (u32 storage, u64 arithmetic).
@@ -21,6 +22,11 @@
 // 2 = __builtin_sub_overflow + select (default: measured fastest in k_rows, tools/kbench)
 #ifndef NTTMUL_CSUB
 #define NTTMUL_CSUB 2
+#endif
+// Arith32 twiddle products: 0 = Shoup (w, floor(w 2^32 / q)), 1 = Montgomery form (planner.cpp
+// emits the matching table pairs; the macro must agree between host and device objects)
+#ifndef NTTMUL_A32_MONT
+#define NTTMUL_A32_MONT 1
 #endif
 
 namespace nttmul {
@@ -55,14 +61,27 @@ struct Arith32 {
 #endif
   }
 
+#if NTTMUL_A32_MONT
+  // x * w mod q in [0, 2q) for any 32-bit x, twiddle in Montgomery form (w1 = w 2^32 mod q,
+  // w2 = w1 (-q^-1) mod 2^32): (x w1 + m q) / 2^32 with m = x w2 mod 2^32 — one v_mul_lo_u32
+  // and two v_mad_u64_u32, no trailing subtraction.  x w1 + m q < 2^33 q < 2^64 for q < 2^31.
+  __device__ __forceinline__ uint32_t shoup(uint32_t x, uint32_t w1, uint32_t w2) const {
+    const uint32_t m = x * w2;
+    const uint64_t s = (uint64_t)x * w1 + (uint64_t)m * q;
+    return (uint32_t)(s >> 32);
+  }
+#else
   // x * w mod q in [0, 2q) for any 32-bit x (Shoup).
   __device__ __forceinline__ uint32_t shoup(uint32_t x, uint32_t w, uint32_t ws) const {
     uint32_t qh = __umulhi(x, ws);
     return x * w - qh * q;
   }
-  // Cooley-Tukey butterfly, ntt.C:365-367 pattern: (X, Y) -> (X + Y w, X - Y w).  In/out [0, 2q).
+#endif
+  // Cooley-Tukey butterfly, ntt.C:365-367 pattern: (X, Y) -> (X + Y w, X - Y w).  In/out [0, 2q);
+  // XC: X is known canonical (the first stage of a transform of canonical input).
+  template <bool XC = false>
   __device__ __forceinline__ void ct(uint32_t &X, uint32_t &Y, uint32_t w, uint32_t ws) const {
-    uint32_t x = csub(X, q);
+    uint32_t x = XC ? X : csub(X, q);
     uint32_t t = csub(shoup(Y, w, ws), q);
     X = x + t;
     Y = x - t + q;
@@ -139,8 +158,9 @@ struct Arith64 {
   }
 #if NTTMUL_A64_PLAIN
   static constexpr uint64_t kLazy = 2;  // values in [0, 2q)
+  template <bool XC = false>
   __device__ __forceinline__ void ct(uint64_t &X, uint64_t &Y, uint64_t w, uint64_t ws) const {
-    uint64_t x = csub(X, q);
+    uint64_t x = XC ? X : csub(X, q);
     uint64_t t = csub(shoup(Y, w, ws), q);
     X = x + t;
     Y = x - t + q;
@@ -160,8 +180,9 @@ struct Arith64 {
 #else
   static constexpr uint64_t kLazy = 4;  // forward values in [0, 4q), inverse values in [0, 2q)
   // Harvey CT: X in [0, 4q), any Y -> outputs in [0, 4q)
+  template <bool XC = false>
   __device__ __forceinline__ void ct(uint64_t &X, uint64_t &Y, uint64_t w, uint64_t ws) const {
-    const uint64_t x = csub(X, 2 * q);
+    const uint64_t x = XC ? X : csub(X, 2 * q);
     const uint64_t t = shoup(Y, w, ws);
     X = x + t;
     Y = x - t + 2 * q;

@@ -15,7 +15,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "launch.hpp"
@@ -27,6 +29,8 @@ using namespace nttmul;
 namespace {
 
 constexpr int kMaxDev = 16;
+constexpr int kSlots = 3;                     // host-path pipeline depth per device
+constexpr size_t kChunkBytes = 8u << 20;      // host-path chunk, per operand
 
 struct DevState {
   int id = -1;
@@ -34,8 +38,12 @@ struct DevState {
   void *fw = nullptr, *iw = nullptr;
   void *scr[3] = {nullptr, nullptr, nullptr};
   size_t scr_bytes = 0;
-  void *io[3] = {nullptr, nullptr, nullptr};  // host-path staging for a, b, c
-  size_t io_bytes = 0;
+  // host-buffer path: kSlots pipeline slots, each with a stream, pinned host staging and device
+  // buffers for a, b, c (run_host)
+  hipStream_t xs[kSlots] = {};
+  void *pin[kSlots][3] = {};
+  void *dbuf[kSlots][3] = {};
+  size_t slot_bytes = 0;
   int *flag = nullptr;                        // range-check result
   int cus = 0;                                // compute units (persistent grid sizing)
 };
@@ -143,41 +151,134 @@ int run_device(nttmul_ctx *ctx, DevState &d, int op, void *c, const void *a, con
   return NTTMUL_OK;
 }
 
+// memcpy split over a few host threads for large blocks (the staging copies bound the
+// host-buffer path: one core moves ~10-20 GB/s, a PCIe Gen5 x16 link ~50 GB/s each way)
+void pcopy(void *dst, const void *src, size_t bytes) {
+  const size_t kPart = 2u << 20;
+  unsigned t = std::thread::hardware_concurrency();
+  t = t ? std::min(t, 8u) : 1u;
+  const size_t parts = std::min<size_t>(t, bytes / kPart);
+  if (parts <= 1) {
+    memcpy(dst, src, bytes);
+    return;
+  }
+  std::vector<std::thread> th;
+  const size_t step = (bytes / parts + 63) & ~(size_t)63;
+  for (size_t i = 1; i < parts; i++) {
+    const size_t o = i * step;
+    if (o >= bytes) break;
+    th.emplace_back(memcpy, (char *)dst + o, (const char *)src + o, std::min(step, bytes - o));
+  }
+  memcpy(dst, src, std::min(step, bytes));
+  for (auto &x : th) x.join();
+}
+
+int ensure_slots(nttmul_ctx *ctx, DevState &d, size_t bytes) {
+  for (int s = 0; s < kSlots; s++)
+    if (!d.xs[s]) HIP_TRY(ctx, hipStreamCreateWithFlags(&d.xs[s], hipStreamNonBlocking));
+  if (d.slot_bytes >= bytes) return NTTMUL_OK;
+  for (int s = 0; s < kSlots; s++) {
+    HIP_TRY(ctx, hipStreamSynchronize(d.xs[s]));
+    for (int k = 0; k < 3; k++) {
+      if (d.pin[s][k]) (void)hipHostFree(d.pin[s][k]);
+      if (d.dbuf[s][k]) (void)hipFree(d.dbuf[s][k]);
+      d.pin[s][k] = d.dbuf[s][k] = nullptr;
+    }
+  }
+  d.slot_bytes = 0;
+  for (int s = 0; s < kSlots; s++)
+    for (int k = 0; k < 3; k++) {
+      HIP_TRY(ctx, hipHostMalloc(&d.pin[s][k], bytes, hipHostMallocDefault));
+      HIP_TRY(ctx, hipMalloc(&d.dbuf[s][k], bytes));
+    }
+  d.slot_bytes = bytes;
+  return NTTMUL_OK;
+}
+
+// Host-buffer path (the FPGA transaction: mode 1/2 DMA in, mode 3, DMA out).  Each device's
+// contiguous slice streams through kSlots pipeline slots in chunks: the host copies
+// chunk j into pinned staging while the GPU runs H2D -> kernel -> D2H of chunks j-1, j-2 on the
+// other slots' streams, and copies a finished chunk's result out when its slot comes round again.
 int run_host(nttmul_ctx *ctx, int op, void *c, const void *a, const void *b, size_t batch,
              int io_bits) {
   const bool two = op == OP_MULTIPLY || op == OP_POINTWISE;
   if (!ctx || !c || !a || (two && !b)) return NTTMUL_EINVAL;
+  if (io_bits != 32 && io_bits != 64) return NTTMUL_EINVAL;
   if (!batch) return NTTMUL_OK;
   DeviceGuard guard;
-  const size_t wb = io_bits / 8, n = ctx->plan.n;
-  // contiguous slices, one per device (no inter-device exchange)
+  const size_t pbytes = (size_t)ctx->plan.n * (io_bits / 8);
+  const size_t chunk = std::max<size_t>(1, kChunkBytes / pbytes);
+  struct Pending {
+    bool busy = false;
+    size_t off = 0, bytes = 0;
+  };
+  struct Job {
+    size_t next = 0, end = 0;
+    unsigned k = 0;
+    Pending slot[kSlots];
+  } job[kMaxDev];
   size_t p0 = 0;
   for (int i = 0; i < ctx->ndev; i++) {
     const size_t p1 = batch * (size_t)(i + 1) / ctx->ndev;
-    const size_t cnt = p1 - p0;
-    DevState &d = ctx->dev[i];
-    if (cnt) {
-      HIP_TRY(ctx, hipSetDevice(d.id));
-      int st = ensure(ctx, d.io, 3, &d.io_bytes, cnt * n * wb);
+    job[i].next = p0;
+    job[i].end = p1;
+    if (p1 > p0) {
+      HIP_TRY(ctx, hipSetDevice(ctx->dev[i].id));
+      int st = ensure_slots(ctx, ctx->dev[i], std::min(chunk, p1 - p0) * pbytes);
       if (st) return st;
-      const size_t off = p0 * n * wb, bytes = cnt * n * wb;
-      HIP_TRY(ctx, hipMemcpyAsync(d.io[0], (const char *)a + off, bytes, hipMemcpyHostToDevice,
-                                  d.stream));
-      if (two)
-        HIP_TRY(ctx, hipMemcpyAsync(d.io[1], (const char *)b + off, bytes,
-                                    hipMemcpyHostToDevice, d.stream));
-      st = run_device(ctx, d, op, d.io[2], d.io[0], d.io[1], cnt, io_bits, d.stream);
-      if (st) return st;
-      HIP_TRY(ctx, hipMemcpyAsync((char *)c + off, d.io[2], bytes, hipMemcpyDeviceToHost,
-                                  d.stream));
     }
     p0 = p1;
   }
-  for (int i = 0; i < ctx->ndev; i++) {
-    HIP_TRY(ctx, hipSetDevice(ctx->dev[i].id));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->dev[i].stream));
+  auto retire = [&](int i, int s) -> int {
+    DevState &d = ctx->dev[i];
+    Pending &pd = job[i].slot[s];
+    if (!pd.busy) return NTTMUL_OK;
+    HIP_TRY(ctx, hipSetDevice(d.id));
+    HIP_TRY(ctx, hipStreamSynchronize(d.xs[s]));
+    pcopy((char *)c + pd.off, d.pin[s][2], pd.bytes);
+    pd.busy = false;
+    return NTTMUL_OK;
+  };
+  int st = NTTMUL_OK;
+  for (bool more = true; more && !st;) {
+    more = false;
+    for (int i = 0; i < ctx->ndev && !st; i++) {
+      Job &J = job[i];
+      if (J.next >= J.end) continue;
+      more = true;
+      DevState &d = ctx->dev[i];
+      const int s = (int)(J.k++ % kSlots);
+      if ((st = retire(i, s))) break;
+      const size_t cnt = std::min(chunk, J.end - J.next);
+      const size_t off = J.next * pbytes, bytes = cnt * pbytes;
+      pcopy(d.pin[s][0], (const char *)a + off, bytes);
+      if (two) pcopy(d.pin[s][1], (const char *)b + off, bytes);
+      hipError_t e = hipMemcpyAsync(d.dbuf[s][0], d.pin[s][0], bytes, hipMemcpyHostToDevice, d.xs[s]);
+      if (e == hipSuccess && two)
+        e = hipMemcpyAsync(d.dbuf[s][1], d.pin[s][1], bytes, hipMemcpyHostToDevice, d.xs[s]);
+      if (e != hipSuccess) {
+        st = fail(ctx, e, "hipMemcpyAsync H2D");
+        break;
+      }
+      if ((st = run_device(ctx, d, op, d.dbuf[s][2], d.dbuf[s][0], d.dbuf[s][1], cnt, io_bits,
+                           d.xs[s])))
+        break;
+      e = hipMemcpyAsync(d.pin[s][2], d.dbuf[s][2], bytes, hipMemcpyDeviceToHost, d.xs[s]);
+      if (e != hipSuccess) {
+        st = fail(ctx, e, "hipMemcpyAsync D2H");
+        break;
+      }
+      J.slot[s] = Pending{true, off, bytes};
+      J.next += cnt;
+    }
   }
-  return NTTMUL_OK;
+  // drain (also after an error, so no slot is left in flight)
+  for (int i = 0; i < ctx->ndev; i++)
+    for (int s = 0; s < kSlots; s++) {
+      int r = retire(i, s);
+      if (!st) st = r;
+    }
+  return st;
 }
 
 }  // namespace
@@ -263,8 +364,15 @@ void nttmul_destroy(nttmul_ctx *ctx) {
     if (d.id < 0) continue;
     (void)hipSetDevice(d.id);
     if (d.stream) (void)hipStreamSynchronize(d.stream);
-    for (void *p : {d.fw, d.iw, (void *)d.flag, d.scr[0], d.scr[1], d.scr[2], d.io[0], d.io[1],
-                    d.io[2]})
+    for (int k = 0; k < kSlots; k++) {
+      if (d.xs[k]) (void)hipStreamSynchronize(d.xs[k]);
+      for (int m = 0; m < 3; m++) {
+        if (d.pin[k][m]) (void)hipHostFree(d.pin[k][m]);
+        if (d.dbuf[k][m]) (void)hipFree(d.dbuf[k][m]);
+      }
+      if (d.xs[k]) (void)hipStreamDestroy(d.xs[k]);
+    }
+    for (void *p : {d.fw, d.iw, (void *)d.flag, d.scr[0], d.scr[1], d.scr[2]})
       if (p) (void)hipFree(p);
     if (d.stream) (void)hipStreamDestroy(d.stream);
   }

@@ -73,14 +73,33 @@ static uint64_t companion(uint64_t w, uint64_t q, int bits) {
   return (uint64_t)(((u128)w << bits) / q);
 }
 
+// (value, companion) pair the device multiplies by: Shoup (w, floor(w 2^bits / q)), or for
+// Arith32 with NTTMUL_A32_MONT the Montgomery form (w 2^32 mod q, that times -q^-1 mod 2^32)
+static void tw_pair(uint64_t w, uint64_t q, int bits, uint64_t *v, uint64_t *c) {
+#if NTTMUL_A32_MONT
+  if (bits == 32) {
+    uint64_t inv = q;
+    for (int i = 0; i < 5; i++) inv *= 2 - q * inv;
+    const uint64_t w1 = (uint64_t)(((u128)w << 32) % q);
+    *v = w1;
+    *c = (w1 * (0 - inv)) & 0xFFFFFFFFull;
+    return;
+  }
+#endif
+  *v = w;
+  *c = companion(w, q, bits);
+}
+
 template <class W>
 static void put_pairs(std::vector<uint8_t> &dst, const std::vector<uint64_t> &w, uint64_t q,
                       int bits) {
   dst.assign(w.size() * 2 * sizeof(W), 0);
   W *p = (W *)dst.data();
   for (size_t i = 0; i < w.size(); i++) {
-    p[2 * i] = (W)w[i];
-    p[2 * i + 1] = (W)companion(w[i], q, bits);
+    uint64_t v, c;
+    tw_pair(w[i], q, bits, &v, &c);
+    p[2 * i] = (W)v;
+    p[2 * i + 1] = (W)c;
   }
 }
 
@@ -173,15 +192,12 @@ int make_plan(uint32_t n, uint64_t q, uint64_t psi, Plan *P, bool cyclic) {
   // F = n^-1 R mod q, R = 2^bits: cancels the Montgomery R^-1 of the pointwise product and the
   // n of the unnormalised inverse transform (ntt256.C:12 scaled_inv_psi_powers' n^-1).
   const uint64_t r_mod_q = (uint64_t)(((u128)1 << bits) % q);
-  P->f = mulmod(P->inv_n, r_mod_q, q);
-  P->fs = companion(P->f, q, bits);
-  P->wf = mulmod(iw[1], P->f, q);
-  P->wfs = companion(P->wf, q, bits);
+  const uint64_t f = mulmod(P->inv_n, r_mod_q, q);
+  tw_pair(f, q, bits, &P->f, &P->fs);
+  tw_pair(mulmod(iw[1], f, q), q, bits, &P->wf, &P->wfs);
   // standalone inverse NTT: plain n^-1 (ntt256.C:12); pointwise product: R^2 mod q
-  P->fi = P->inv_n;
-  P->fis = companion(P->fi, q, bits);
-  P->wfi = mulmod(iw[1], P->fi, q);
-  P->wfis = companion(P->wfi, q, bits);
+  tw_pair(P->inv_n, q, bits, &P->fi, &P->fis);
+  tw_pair(mulmod(iw[1], P->inv_n, q), q, bits, &P->wfi, &P->wfis);
   P->r2 = mulmod(r_mod_q, r_mod_q, q);
   return NTTMUL_OK;
 }

@@ -11,6 +11,11 @@
 
 #include <vector>
 
+// Arith32 twiddle form (see modarith.hpp); host tables and device kernels must agree
+#ifndef NTTMUL_A32_MONT
+#define NTTMUL_A32_MONT 1
+#endif
+
 namespace nttmul {
 
 uint64_t mulmod(uint64_t a, uint64_t b, uint64_t q);
