@@ -28,6 +28,10 @@
 #ifndef NTTMUL_LDS_REGIONS
 #define NTTMUL_LDS_REGIONS 2
 #endif
+// Arith32H (Harvey bounds) for q < 2^30
+#ifndef NTTMUL_A32H
+#define NTTMUL_A32H 1
+#endif
 // skip the reduction of X in the first forward stage (input canonical by contract)
 #ifndef NTTMUL_FIRST_XC
 #define NTTMUL_FIRST_XC 1
@@ -519,6 +523,13 @@ static hipError_t multipass(const LaunchTables &T, const void *a, const void *b,
 hipError_t launch_polymul(const LaunchTables &T, const void *a, const void *b, void *c,
                           size_t batch, int io_bits, void **scr, hipStream_t s) {
   const bool big = T.logn > 12;
+  if (NTTMUL_A32H && T.word_bits == 32 && T.q < (1ull << 30)) {  // Harvey bounds fit
+    if (io_bits == 64)
+      return big ? multipass<Arith32H, uint64_t>(T, a, b, c, batch, scr, s)
+                 : fused<Arith32H, uint64_t>(T, a, b, c, batch, s);
+    return big ? multipass<Arith32H, uint32_t>(T, a, b, c, batch, scr, s)
+               : fused<Arith32H, uint32_t>(T, a, b, c, batch, s);
+  }
   if (T.word_bits == 32) {
     if (io_bits == 64)  // 64-bit storage of a q < 2^31 product: same 32-bit arithmetic
       return big ? multipass<Arith32, uint64_t>(T, a, b, c, batch, scr, s)
@@ -606,6 +617,9 @@ static hipError_t xform_any(const LaunchTables &T, const void *in, void *out, si
 template <int DIR>
 static hipError_t launch_xform_dir(const LaunchTables &T, const void *in, void *out, size_t batch,
                                    int io_bits, void **scr, hipStream_t s) {
+  if (NTTMUL_A32H && T.word_bits == 32 && T.q < (1ull << 30))
+    return io_bits == 64 ? xform_any<Arith32H, uint64_t, DIR>(T, in, out, batch, scr, s)
+                         : xform_any<Arith32H, uint32_t, DIR>(T, in, out, batch, scr, s);
   if (T.word_bits == 32)
     return io_bits == 64 ? xform_any<Arith32, uint64_t, DIR>(T, in, out, batch, scr, s)
                          : xform_any<Arith32, uint32_t, DIR>(T, in, out, batch, scr, s);

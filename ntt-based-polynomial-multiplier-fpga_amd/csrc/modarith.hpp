@@ -31,7 +31,11 @@
 
 namespace nttmul {
 
-struct Arith32 {
+// H (Harvey lazy bounds, q < 2^30): forward values in [0, 4q), inverse values in [0, 2q), one
+// conditional subtraction per butterfly instead of two.  Without H (q < 2^31) there is no
+// headroom above 2q in a 32-bit word and every butterfly reduces both of its operands.
+template <bool H>
+struct Arith32T {
   using word = uint32_t;
   static constexpr int kBits = 32;
   uint32_t q;
@@ -79,8 +83,16 @@ struct Arith32 {
 #endif
   // Cooley-Tukey butterfly, ntt.C:365-367 pattern: (X, Y) -> (X + Y w, X - Y w).  In/out [0, 2q);
   // XC: X is known canonical (the first stage of a transform of canonical input).
+  // (H: X in [0, 4q), outputs in [0, 4q).)
   template <bool XC = false>
   __device__ __forceinline__ void ct(uint32_t &X, uint32_t &Y, uint32_t w, uint32_t ws) const {
+    if (H) {
+      const uint32_t x = XC ? X : csub(X, 2 * q);
+      const uint32_t t = shoup(Y, w, ws);
+      X = x + t;
+      Y = x - t + 2 * q;
+      return;
+    }
     uint32_t x = XC ? X : csub(X, q);
     uint32_t t = csub(shoup(Y, w, ws), q);
     X = x + t;
@@ -88,6 +100,12 @@ struct Arith32 {
   }
   // Gentleman-Sande butterfly, ntt.C:445-447 pattern: (X, Y) -> (X + Y, (X - Y) w).  In/out [0, 2q).
   __device__ __forceinline__ void gs(uint32_t &X, uint32_t &Y, uint32_t w, uint32_t ws) const {
+    if (H) {
+      const uint32_t x = X, y = Y;
+      X = csub(x + y, 2 * q);
+      Y = shoup(x - y + 2 * q, w, ws);
+      return;
+    }
     uint32_t x = csub(X, q), y = csub(Y, q);
     X = x + y;
     Y = shoup(x - y + q, w, ws);
@@ -95,19 +113,33 @@ struct Arith32 {
   // Last inverse stage with the output scale F folded in: (X, Y) -> ((X + Y) F, (X - Y) w F).
   __device__ __forceinline__ void gs_scaled(uint32_t &X, uint32_t &Y, uint32_t f, uint32_t fs,
                                             uint32_t wf, uint32_t wfs) const {
+    if (H) {
+      const uint32_t x = X, y = Y;
+      X = shoup(x + y, f, fs);
+      Y = shoup(x - y + 2 * q, wf, wfs);
+      return;
+    }
     uint32_t x = csub(X, q), y = csub(Y, q);
     X = shoup(x + y, f, fs);
     Y = shoup(x - y + q, wf, wfs);
   }
-  // Montgomery product a b 2^-32 mod q, inputs in [0, 2q), output in [0, 2q).
+  // Montgomery product a b 2^-32 mod q, inputs lazy (H: < 4q, else < 2q), output in [0, 2q):
+  // both reduced below 2q first, t + m q < 4 q^2 + 2^32 q < 2^64.
   __device__ __forceinline__ uint32_t mont(uint32_t a, uint32_t b) const {
-    uint64_t t = (uint64_t)csub(a, q) * csub(b, q);  // < q^2
+    const uint32_t m2 = H ? 2 * q : q;
+    const uint32_t ar = H ? csub(a, m2) : csub(a, q), br = H ? csub(b, m2) : csub(b, q);
+    uint64_t t = (uint64_t)ar * br;
     uint32_t m = (uint32_t)t * qinv_neg;
-    uint64_t u = t + (uint64_t)m * q;                // < q^2 + 2^32 q < 2^64
+    uint64_t u = t + (uint64_t)m * q;
     return (uint32_t)(u >> 32);
   }
-  __device__ __forceinline__ uint32_t canon(uint32_t x) const { return csub(x, q); }
+  // lazy -> [0, q)
+  __device__ __forceinline__ uint32_t canon(uint32_t x) const {
+    return H ? csub(csub(x, 2 * q), q) : csub(x, q);
+  }
 };
+using Arith32 = Arith32T<false>;   // q < 2^31
+using Arith32H = Arith32T<true>;   // q < 2^30
 
 // 64-bit arithmetic on a 32-bit VALU.  q < 2^62 leaves two bits of headroom, so butterflies use
 // Harvey's lazy bounds (values in [0, 4q), one conditional subtraction per butterfly instead of

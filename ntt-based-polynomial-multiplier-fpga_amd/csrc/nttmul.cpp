@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -152,26 +153,72 @@ int run_device(nttmul_ctx *ctx, DevState &d, int op, void *c, const void *a, con
 }
 
 // memcpy split over a few host threads for large blocks (the staging copies bound the
-// host-buffer path: one core moves ~10-20 GB/s, a PCIe Gen5 x16 link ~50 GB/s each way)
-void pcopy(void *dst, const void *src, size_t bytes) {
-  const size_t kPart = 2u << 20;
-  unsigned t = std::thread::hardware_concurrency();
-  t = t ? std::min(t, 8u) : 1u;
-  const size_t parts = std::min<size_t>(t, bytes / kPart);
-  if (parts <= 1) {
-    memcpy(dst, src, bytes);
-    return;
+// host-buffer path: one core moves ~10-20 GB/s, a PCIe Gen5 x16 link ~50 GB/s each way).  The
+// workers are started once and live for the process (never joined: the pool is never freed).
+class CopyPool {
+ public:
+  static CopyPool &get() {
+    static CopyPool *pool = new CopyPool();
+    return *pool;
   }
-  std::vector<std::thread> th;
-  const size_t step = (bytes / parts + 63) & ~(size_t)63;
-  for (size_t i = 1; i < parts; i++) {
-    const size_t o = i * step;
-    if (o >= bytes) break;
-    th.emplace_back(memcpy, (char *)dst + o, (const char *)src + o, std::min(step, bytes - o));
+  void copy(void *dst, const void *src, size_t bytes) {
+    const size_t kPart = 1u << 20;
+    const size_t parts = std::min<size_t>(workers_ + 1, bytes / kPart);
+    if (parts <= 1) {
+      memcpy(dst, src, bytes);
+      return;
+    }
+    std::unique_lock<std::mutex> call(call_mu_);  // one split copy at a time
+    const size_t step = (bytes / parts + 4095) & ~(size_t)4095;
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      d_ = (char *)dst;
+      s_ = (const char *)src;
+      bytes_ = bytes;
+      step_ = step;
+      pending_ = parts - 1;
+      used_ = parts - 1;
+      gen_++;
+    }
+    cv_.notify_all();
+    memcpy(dst, src, std::min(step, bytes));
+    std::unique_lock<std::mutex> l(mu_);
+    done_.wait(l, [&] { return pending_ == 0; });
   }
-  memcpy(dst, src, std::min(step, bytes));
-  for (auto &x : th) x.join();
-}
+
+ private:
+  CopyPool() {
+    unsigned hw = std::thread::hardware_concurrency();
+    workers_ = hw > 1 ? std::min(hw - 1, 7u) : 0;
+    for (unsigned i = 0; i < workers_; i++) std::thread([this, i] { run(i); }).detach();
+  }
+  void run(unsigned i) {
+    unsigned seen = 0;
+    for (;;) {
+      std::unique_lock<std::mutex> l(mu_);
+      cv_.wait(l, [&] { return gen_ != seen; });
+      seen = gen_;
+      if (i >= used_) continue;
+      const size_t o = (i + 1) * step_;
+      char *d = d_;
+      const char *s = s_;
+      const size_t len = o < bytes_ ? std::min(step_, bytes_ - o) : 0;
+      l.unlock();
+      if (len) memcpy(d + o, s + o, len);
+      l.lock();
+      if (--pending_ == 0) done_.notify_one();
+    }
+  }
+  unsigned workers_ = 0;
+  std::mutex call_mu_, mu_;
+  std::condition_variable cv_, done_;
+  unsigned gen_ = 0;
+  size_t pending_ = 0, used_ = 0, bytes_ = 0, step_ = 0;
+  char *d_ = nullptr;
+  const char *s_ = nullptr;
+};
+
+void pcopy(void *dst, const void *src, size_t bytes) { CopyPool::get().copy(dst, src, bytes); }
 
 int ensure_slots(nttmul_ctx *ctx, DevState &d, size_t bytes) {
   for (int s = 0; s < kSlots; s++)

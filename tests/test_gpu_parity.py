@@ -122,7 +122,7 @@ def test_random_vs_oracle(n, q, torch_cuda):
 
 
 @pytest.mark.parametrize("n", [8192, 16384, 32768, 65536])
-@pytest.mark.parametrize("q", [Q31, Q62])
+@pytest.mark.parametrize("q", [Q31, Q30, Q62])
 def test_multipass_vs_oracle(n, q, torch_cuda):
     """n > 4096: column pass + fused rows + inverse column pass."""
     P = O.Plan(n, q)
@@ -229,7 +229,7 @@ def test_transforms_ref256_golden(golden_dir, torch_cuda):
 
 
 @pytest.mark.parametrize("n", [256, 1024, 4096, 8192, 65536])
-@pytest.mark.parametrize("q", [Q31, Q62])
+@pytest.mark.parametrize("q", [Q31, Q30, Q62])
 def test_transforms_vs_oracle(n, q, torch_cuda):
     P = O.Plan(n, q)
     ctx = _ctx(n, q)
@@ -295,7 +295,8 @@ def test_cyclic_fpga_vectors(golden_dir, torch_cuda):
     assert list(ctx.multiply(a, b)[:5]) == [2, 6, 10, 6, 0]
 
 
-@pytest.mark.parametrize("n,q", [(1024, Q31), (4096, Q31), (8192, Q31), (2048, Q62)])
+@pytest.mark.parametrize("n,q", [(1024, Q31), (4096, Q31), (8192, Q31), (4096, Q30), (8192, Q30),
+                                 (2048, Q62)])
 def test_cyclic_vs_schoolbook(n, q, torch_cuda):
     ctx = _ctx(n, q, cyclic=True)
     a, b = O.fill_inputs(n, q, 3, 2)
@@ -318,3 +319,18 @@ def test_time_testing_gpu_app(golden_dir, torch_cuda):
     vals = [int(x) for line in out.split("Resultado C = A * B):")[1].split("\n") for x in line.split()]
     assert vals == [int(v) for v in g["ntt256_product4"][0]]
     assert "Batch 1024" in out
+
+
+@pytest.mark.parametrize("n,q,batch", [(4096, Q31, 1537), (256, Q30, 20000), (1024, Q62, 1100)])
+def test_host_path_pipeline(n, q, batch, torch_cuda):
+    """The host-buffer ABI path streams 8 MiB chunks through 3 pipeline slots (nttmul.cpp
+    run_host): several chunks, a partial last chunk and slot reuse, every product checked."""
+    ctx = _ctx(n, q)
+    a, b = O.fill_inputs(n, q, 11, batch)
+    dt = np.uint32 if q < (1 << 32) else np.uint64
+    c = ctx.multiply(a.astype(dt), b.astype(dt)).astype(np.uint64)
+    ref = O.Plan(n, q).product_batch(a, b)[0]
+    assert np.array_equal(c, ref.reshape(batch, n))
+    # the standalone transforms take the same path
+    fa = ctx.forward(a.astype(dt))
+    assert np.array_equal(ctx.inverse(fa).astype(np.uint64), a)
