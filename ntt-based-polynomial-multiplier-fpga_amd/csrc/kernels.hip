@@ -28,6 +28,10 @@
 #ifndef NTTMUL_LDS_REGIONS
 #define NTTMUL_LDS_REGIONS 2
 #endif
+// non-temporal loads/stores of the coefficient streams in k_rows
+#ifndef NTTMUL_NT
+#define NTTMUL_NT 1
+#endif
 // Arith32H (Harvey bounds) for q < 2^30
 #ifndef NTTMUL_A32H
 #define NTTMUL_A32H 1
@@ -112,6 +116,24 @@ struct Groups {
 
 template <class W, class T>
 __device__ __forceinline__ W to_word(T v) { return (W)v; }
+
+// Coefficient streams are touched once per product: NTTMUL_NT marks them non-temporal
+template <class T>
+__device__ __forceinline__ T ld_stream(const T *p) {
+#if NTTMUL_NT
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
+template <class T>
+__device__ __forceinline__ void st_stream(T *p, T v) {
+#if NTTMUL_NT
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
 
 // Forward CT stages of group g on NPOLY (1 or 2) polynomials (same twiddles).
 template <class A, int LOGS, int g, int NPOLY = 2>
@@ -269,8 +291,8 @@ __global__ __launch_bounds__(256, NTTMUL_MIN_WAVES) void k_rows(KParams<A> P, co
 #else
 #pragma unroll
   for (int k = 0; k < 16; k++) {
-    x[k] = to_word<W>(a[base_l + Gr::off(0, k)]);
-    y[k] = to_word<W>(b[base_l + Gr::off(0, k)]);
+    x[k] = to_word<W>(ld_stream(a + base_l + Gr::off(0, k)));
+    y[k] = to_word<W>(ld_stream(b + base_l + Gr::off(0, k)));
   }
 #endif
   W *lx = lds[pb][0], *ly = lds[pb][NTTMUL_LDS_REGIONS - 1];
@@ -290,7 +312,7 @@ __global__ __launch_bounds__(256, NTTMUL_MIN_WAVES) void k_rows(KParams<A> P, co
     for (int k = 0; k < 16; k++) {
       W v = x[k];
       if (L1 == 0) v = P.ar.canon(v);
-      c[base_g + Gr::off(0, k)] = (TOut)v;
+      st_stream(c + base_g + Gr::off(0, k), (TOut)v);
     }
   }
 }
