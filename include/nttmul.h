@@ -124,6 +124,30 @@ int nttmul_inverse_batch_device(nttmul_ctx *ctx, void *out, const void *in, size
 int nttmul_pointwise_batch_device(nttmul_ctx *ctx, void *c, const void *a, const void *b,
                                   size_t batch, int word_bits, int dev, void *stream);
 
+/* General transform entry point: the reference's whole wrapper set (NTT/ntt256.h:20-69) for any
+ * context.  mode = direction | order | scaling:
+ *   NTTMUL_XF_FORWARD / NTTMUL_XF_INVERSE
+ *   NTTMUL_XF_STD2REV : standard-order input, bit-reversed output (ntt_ct/gs_std2rev)
+ *   NTTMUL_XF_REV2STD : bit-reversed input, standard-order output (ntt_ct/gs_rev2std)
+ *   NTTMUL_XF_UNSCALED: inverse without n^-1, as the reference's intt* / inttmul* (ntt256.h:16-17:
+ *                       intt(ntt(a)) = n a)
+ * On a negacyclic context the forward is mulntt (psi weights merged, ntt.C:257-371) and the
+ * inverse nttmul / inttmul (psi^-1 merged, ntt.C:387-493); on a NTTMUL_FLAG_CYCLIC context they
+ * are the plain ntt / intt with omega.  The CT and GS loops of the reference give identical
+ * results for the same order, so there is one entry per (direction, order, scaling).
+ * nttmul_forward_* == FORWARD | STD2REV, nttmul_inverse_* == INVERSE | REV2STD. */
+#define NTTMUL_XF_FORWARD 0u
+#define NTTMUL_XF_INVERSE 1u
+#define NTTMUL_XF_STD2REV 0u
+#define NTTMUL_XF_REV2STD 2u
+#define NTTMUL_XF_UNSCALED 4u
+int nttmul_transform_batch_u32(nttmul_ctx *ctx, unsigned mode, uint32_t *out, const uint32_t *in,
+                               size_t batch);
+int nttmul_transform_batch_u64(nttmul_ctx *ctx, unsigned mode, uint64_t *out, const uint64_t *in,
+                               size_t batch);
+int nttmul_transform_device(nttmul_ctx *ctx, unsigned mode, void *out, const void *in,
+                            size_t batch, int word_bits, int dev, void *stream);
+
 /* Synthetic inputs on the device: a[p][i] = splitmix64(seed + 2n(p0+p) + i) mod q,
  * b[p][i] = splitmix64(seed + 2n(p0+p) + n + i) mod q, for p in [0, count).  Asynchronous. */
 int nttmul_fill_random_device(nttmul_ctx *ctx, void *a, void *b, uint64_t p0, size_t count,
@@ -179,6 +203,24 @@ void ntt256_product1(int32_t *c, int32_t *a, int32_t *b);
 void ntt256_product4(int32_t *c, int32_t *a, int32_t *b);
 void ntt_red256_product1(int32_t *c, int32_t *a, int32_t *b);
 void ntt_red256_product4(int32_t *c, int32_t *a, int32_t *b);
+
+/* The reference's n = 256 transform wrappers (NTT/ntt256.h:20-69, there static inline over the
+ * ntt.C loops and the ntt256_tables.C tables), in place on int32 a[256] in [0, q-1], same names
+ * and results: ntt256_* forward and intt256_* unscaled inverse with omega = psi^2 = 8595
+ * (cyclic), mulntt256_* forward with psi merged, inttmul256_* unscaled inverse with psi^-1
+ * merged.  A program that included ntt256.h replaces it with this header. */
+void ntt256_ct_rev2std(int32_t *a);
+void ntt256_gs_rev2std(int32_t *a);
+void ntt256_ct_std2rev(int32_t *a);
+void ntt256_gs_std2rev(int32_t *a);
+void intt256_ct_rev2std(int32_t *a);
+void intt256_gs_rev2std(int32_t *a);
+void intt256_ct_std2rev(int32_t *a);
+void intt256_gs_std2rev(int32_t *a);
+void mulntt256_ct_rev2std(int32_t *a);
+void mulntt256_ct_std2rev(int32_t *a);
+void inttmul256_gs_rev2std(int32_t *a);
+void inttmul256_gs_std2rev(int32_t *a);
 
 #ifdef __cplusplus
 }

@@ -462,6 +462,29 @@ __global__ void k_fill(T *a, T *b, uint32_t logn, uint64_t q, uint64_t seed, uin
   b[i] = (T)(splitmix64(base + n + k) % q);
 }
 
+// Bit-reversal permutation of each polynomial (NTT/ntt.C:27-44 bitrev_shuffle): turns the
+// std2rev transforms into the reference's rev2std variants and back (ntt256.h:20-69).
+template <class T>
+__global__ void k_bitrev(const T *__restrict__ in, T *__restrict__ out, uint32_t logn,
+                         size_t total) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const size_t e = i & ((1u << logn) - 1), p = i - e;
+  out[p + (__brev((uint32_t)e) >> (32 - logn))] = in[i];
+}
+template <class T>
+__global__ void k_bitrev_inplace(T *a, uint32_t logn, size_t total) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const size_t e = i & ((1u << logn) - 1), p = i - e;
+  const size_t r = __brev((uint32_t)e) >> (32 - logn);
+  if (e < r) {
+    const T t = a[p + e];
+    a[p + e] = a[p + r];
+    a[p + r] = t;
+  }
+}
+
 template <class T>
 __global__ void k_check_range(const T *a, const T *b, uint64_t q, size_t total, int *bad) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -675,6 +698,28 @@ hipError_t launch_pointwise(const LaunchTables &T, const void *a, const void *b,
                          : pointwise<Arith32, uint32_t>(T, a, b, c, total, s);
   return io_bits == 64 ? pointwise<Arith64, uint64_t>(T, a, b, c, total, s)
                        : pointwise<Arith64, uint32_t>(T, a, b, c, total, s);
+}
+
+hipError_t launch_bitrev(const void *in, void *out, uint32_t logn, size_t batch, int io_bits,
+                         hipStream_t s) {
+  const size_t total = batch << logn;
+  if (!total) return hipSuccess;
+  const unsigned blocks = (unsigned)((total + 255) / 256);
+  if (in == out) {
+    if (io_bits == 32)
+      hipLaunchKernelGGL(k_bitrev_inplace<uint32_t>, dim3(blocks), dim3(256), 0, s, (uint32_t *)out,
+                         logn, total);
+    else
+      hipLaunchKernelGGL(k_bitrev_inplace<uint64_t>, dim3(blocks), dim3(256), 0, s, (uint64_t *)out,
+                         logn, total);
+  } else if (io_bits == 32) {
+    hipLaunchKernelGGL(k_bitrev<uint32_t>, dim3(blocks), dim3(256), 0, s, (const uint32_t *)in,
+                       (uint32_t *)out, logn, total);
+  } else {
+    hipLaunchKernelGGL(k_bitrev<uint64_t>, dim3(blocks), dim3(256), 0, s, (const uint64_t *)in,
+                       (uint64_t *)out, logn, total);
+  }
+  return hipGetLastError();
 }
 
 hipError_t launch_fill(void *a, void *b, uint32_t logn, uint64_t q, uint64_t seed, uint64_t p0,

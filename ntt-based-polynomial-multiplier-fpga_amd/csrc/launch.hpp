@@ -30,6 +30,9 @@ hipError_t launch_xform(const LaunchTables &T, const void *in, void *out, size_t
 // c = a * b mod q coefficient-wise over batch * n words.
 hipError_t launch_pointwise(const LaunchTables &T, const void *a, const void *b, void *c,
                             size_t batch, int io_bits, hipStream_t s);
+// Bit-reversal permutation of each of `batch` polynomials of 2^logn words (in == out: in place).
+hipError_t launch_bitrev(const void *in, void *out, uint32_t logn, size_t batch, int io_bits,
+                         hipStream_t s);
 hipError_t launch_fill(void *a, void *b, uint32_t logn, uint64_t q, uint64_t seed, uint64_t p0,
                        size_t count, int io_bits, hipStream_t s);
 hipError_t launch_check_range(const void *a, const void *b, uint64_t q, size_t total, int io_bits,

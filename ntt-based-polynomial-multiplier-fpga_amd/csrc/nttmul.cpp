@@ -39,6 +39,8 @@ struct DevState {
   void *fw = nullptr, *iw = nullptr;
   void *scr[3] = {nullptr, nullptr, nullptr};
   size_t scr_bytes = 0;
+  void *perm = nullptr;                       // bit-reversed copy of a transform's input
+  size_t perm_bytes = 0;
   // host-buffer path: kSlots pipeline slots, each with a stream, pinned host staging and device
   // buffers for a, b, c (run_host)
   hipStream_t xs[kSlots] = {};
@@ -114,7 +116,15 @@ int ensure(nttmul_ctx *ctx, void **bufs, int nb, size_t *have, size_t need) {
   return NTTMUL_OK;
 }
 
-enum Op { OP_MULTIPLY = 0, OP_FORWARD = 1, OP_INVERSE = 2, OP_POINTWISE = 3 };
+// Transforms are OP_XFORM + an NTTMUL_XF_* mode (direction | order | scaling).
+enum Op {
+  OP_MULTIPLY = 0,
+  OP_POINTWISE = 3,
+  OP_XFORM = 16,
+  OP_FORWARD = OP_XFORM + (NTTMUL_XF_FORWARD | NTTMUL_XF_STD2REV),
+  OP_INVERSE = OP_XFORM + (NTTMUL_XF_INVERSE | NTTMUL_XF_REV2STD),
+};
+constexpr unsigned kXfModes = NTTMUL_XF_INVERSE | NTTMUL_XF_REV2STD | NTTMUL_XF_UNSCALED;
 
 // Enqueue one device-resident batch of `op` on d (current device must be d.id).  b is unused by
 // the transforms.
@@ -141,11 +151,31 @@ int run_device(nttmul_ctx *ctx, DevState &d, int op, void *c, const void *a, con
     int st = ensure(ctx, d.scr, 3, &d.scr_bytes, need);
     if (st) return st;
   }
-  const LaunchTables T = tables_for(ctx, d);
+  LaunchTables T = tables_for(ctx, d);
+  if (op >= OP_XFORM) {
+    const unsigned mode = (unsigned)(op - OP_XFORM);
+    if (mode & ~kXfModes) return NTTMUL_EINVAL;
+    const bool inv = mode & NTTMUL_XF_INVERSE, rev_in = mode & NTTMUL_XF_REV2STD;
+    if (mode & NTTMUL_XF_UNSCALED) {
+      if (!inv) return NTTMUL_EINVAL;
+      T.fi = P.fu; T.fis = P.fus; T.wfi = P.wfu; T.wfis = P.wfus;
+    }
+    // the kernels run forward std2rev and inverse rev2std; the other orders are the same
+    // transform between two bit-reversal permutations (rev2std = P o std2rev o P, verified on
+    // the reference's own loops: tests/golden/ref256_wrappers.npz)
+    if (inv == rev_in) {
+      HIP_TRY(ctx, launch_xform(T, a, c, batch, io_bits, inv, d.scr, s));
+    } else {
+      int st = ensure(ctx, &d.perm, 1, &d.perm_bytes, batch * (size_t)P.n * (io_bits / 8));
+      if (st) return st;
+      HIP_TRY(ctx, launch_bitrev(a, d.perm, P.logn, batch, io_bits, s));
+      HIP_TRY(ctx, launch_xform(T, d.perm, c, batch, io_bits, inv, d.scr, s));
+      HIP_TRY(ctx, launch_bitrev(c, c, P.logn, batch, io_bits, s));
+    }
+    return NTTMUL_OK;
+  }
   switch (op) {
     case OP_MULTIPLY: HIP_TRY(ctx, launch_polymul(T, a, b, c, batch, io_bits, d.scr, s)); break;
-    case OP_FORWARD: HIP_TRY(ctx, launch_xform(T, a, c, batch, io_bits, 0, d.scr, s)); break;
-    case OP_INVERSE: HIP_TRY(ctx, launch_xform(T, a, c, batch, io_bits, 1, d.scr, s)); break;
     case OP_POINTWISE: HIP_TRY(ctx, launch_pointwise(T, a, b, c, batch, io_bits, s)); break;
     default: return NTTMUL_EINVAL;
   }
@@ -419,7 +449,7 @@ void nttmul_destroy(nttmul_ctx *ctx) {
       }
       if (d.xs[k]) (void)hipStreamDestroy(d.xs[k]);
     }
-    for (void *p : {d.fw, d.iw, (void *)d.flag, d.scr[0], d.scr[1], d.scr[2]})
+    for (void *p : {d.fw, d.iw, (void *)d.flag, d.scr[0], d.scr[1], d.scr[2], d.perm})
       if (p) (void)hipFree(p);
     if (d.stream) (void)hipStreamDestroy(d.stream);
   }
@@ -470,6 +500,16 @@ int nttmul_inverse_batch_u32(nttmul_ctx *ctx, uint32_t *out, const uint32_t *in,
 int nttmul_inverse_batch_u64(nttmul_ctx *ctx, uint64_t *out, const uint64_t *in, size_t batch) {
   return run_host(ctx, OP_INVERSE, out, in, nullptr, batch, 64);
 }
+int nttmul_transform_batch_u32(nttmul_ctx *ctx, unsigned mode, uint32_t *out, const uint32_t *in,
+                               size_t batch) {
+  if (mode & ~kXfModes) return NTTMUL_EINVAL;
+  return run_host(ctx, OP_XFORM + (int)mode, out, in, nullptr, batch, 32);
+}
+int nttmul_transform_batch_u64(nttmul_ctx *ctx, unsigned mode, uint64_t *out, const uint64_t *in,
+                               size_t batch) {
+  if (mode & ~kXfModes) return NTTMUL_EINVAL;
+  return run_host(ctx, OP_XFORM + (int)mode, out, in, nullptr, batch, 64);
+}
 int nttmul_pointwise_batch_u32(nttmul_ctx *ctx, uint32_t *c, const uint32_t *a,
                                const uint32_t *b, size_t batch) {
   return run_host(ctx, OP_POINTWISE, c, a, b, batch, 32);
@@ -502,6 +542,11 @@ int nttmul_inverse_batch_device(nttmul_ctx *ctx, void *out, const void *in, size
                                 int word_bits, int dev, void *stream) {
   return device_op(ctx, OP_INVERSE, out, in, nullptr, batch, word_bits, dev, stream);
 }
+int nttmul_transform_device(nttmul_ctx *ctx, unsigned mode, void *out, const void *in,
+                            size_t batch, int word_bits, int dev, void *stream) {
+  if (mode & ~kXfModes) return NTTMUL_EINVAL;
+  return device_op(ctx, OP_XFORM + (int)mode, out, in, nullptr, batch, word_bits, dev, stream);
+}
 int nttmul_pointwise_batch_device(nttmul_ctx *ctx, void *c, const void *a, const void *b,
                                   size_t batch, int word_bits, int dev, void *stream) {
   return device_op(ctx, OP_POINTWISE, c, a, b, batch, word_bits, dev, stream);
@@ -523,28 +568,45 @@ int nttmul_fill_random_device(nttmul_ctx *ctx, void *a, void *b, uint64_t p0, si
 // ---------------------------------------------------------------------------------------------
 // Compat shims: the reference's software-path entry points (n = 256, q = 12289, psi = 1002).
 // ---------------------------------------------------------------------------------------------
-static nttmul_ctx *g_ctx256 = nullptr;
-static std::once_flag g_once256;
+static nttmul_ctx *g_ctx256[2] = {nullptr, nullptr};  // [0] negacyclic psi, [1] cyclic omega
+static std::once_flag g_once256[2];
 static std::mutex g_mu256;
 
-static void product256(int32_t *c, const int32_t *a, const int32_t *b) {
-  std::call_once(g_once256, [] {
+static nttmul_ctx *ctx256(int cyclic) {
+  std::call_once(g_once256[cyclic], [cyclic] {
     nttmul_params p;
     memset(&p, 0, sizeof(p));
     p.n = 256;
     p.q = 12289;
-    p.psi = 1002;  // ntt256_tables.h:20
+    // ntt256_tables.h:20-24: psi = 1002, omega = psi^2 = 8595
+    p.psi = cyclic ? 8595 : 1002;
+    p.flags = cyclic ? NTTMUL_FLAG_CYCLIC : 0;
     p.ndev = 1;
-    int st = nttmul_create_ex(&g_ctx256, &p);
+    int st = nttmul_create_ex(&g_ctx256[cyclic], &p);
     if (st) {
       fprintf(stderr, "nttmul: ntt256 context: %s\n", nttmul_strerror(st));
       abort();
     }
   });
+  return g_ctx256[cyclic];
+}
+
+static void product256(int32_t *c, const int32_t *a, const int32_t *b) {
+  nttmul_ctx *ctx = ctx256(0);
   std::lock_guard<std::mutex> lock(g_mu256);
-  int st = nttmul_multiply_u32(g_ctx256, (uint32_t *)c, (const uint32_t *)a, (const uint32_t *)b);
+  int st = nttmul_multiply_u32(ctx, (uint32_t *)c, (const uint32_t *)a, (const uint32_t *)b);
   if (st) {
-    fprintf(stderr, "nttmul: ntt256 product: %s (%s)\n", nttmul_strerror(st), g_ctx256->err);
+    fprintf(stderr, "nttmul: ntt256 product: %s (%s)\n", nttmul_strerror(st), ctx->err);
+    abort();
+  }
+}
+
+static void transform256(int32_t *a, int cyclic, unsigned mode) {
+  nttmul_ctx *ctx = ctx256(cyclic);
+  std::lock_guard<std::mutex> lock(g_mu256);
+  int st = nttmul_transform_batch_u32(ctx, mode, (uint32_t *)a, (const uint32_t *)a, 1);
+  if (st) {
+    fprintf(stderr, "nttmul: ntt256 transform: %s (%s)\n", nttmul_strerror(st), ctx->err);
     abort();
   }
 }
@@ -553,5 +615,23 @@ void ntt256_product1(int32_t *c, int32_t *a, int32_t *b) { product256(c, a, b); 
 void ntt256_product4(int32_t *c, int32_t *a, int32_t *b) { product256(c, a, b); }
 void ntt_red256_product1(int32_t *c, int32_t *a, int32_t *b) { product256(c, a, b); }
 void ntt_red256_product4(int32_t *c, int32_t *a, int32_t *b) { product256(c, a, b); }
+
+// NTT/ntt256.h:20-69 (CT and GS of the same order compute the same transform)
+constexpr unsigned kFwdR2S = NTTMUL_XF_FORWARD | NTTMUL_XF_REV2STD;
+constexpr unsigned kFwdS2R = NTTMUL_XF_FORWARD | NTTMUL_XF_STD2REV;
+constexpr unsigned kInvR2S = NTTMUL_XF_INVERSE | NTTMUL_XF_REV2STD | NTTMUL_XF_UNSCALED;
+constexpr unsigned kInvS2R = NTTMUL_XF_INVERSE | NTTMUL_XF_STD2REV | NTTMUL_XF_UNSCALED;
+void ntt256_ct_rev2std(int32_t *a) { transform256(a, 1, kFwdR2S); }
+void ntt256_gs_rev2std(int32_t *a) { transform256(a, 1, kFwdR2S); }
+void ntt256_ct_std2rev(int32_t *a) { transform256(a, 1, kFwdS2R); }
+void ntt256_gs_std2rev(int32_t *a) { transform256(a, 1, kFwdS2R); }
+void intt256_ct_rev2std(int32_t *a) { transform256(a, 1, kInvR2S); }
+void intt256_gs_rev2std(int32_t *a) { transform256(a, 1, kInvR2S); }
+void intt256_ct_std2rev(int32_t *a) { transform256(a, 1, kInvS2R); }
+void intt256_gs_std2rev(int32_t *a) { transform256(a, 1, kInvS2R); }
+void mulntt256_ct_rev2std(int32_t *a) { transform256(a, 0, kFwdR2S); }
+void mulntt256_ct_std2rev(int32_t *a) { transform256(a, 0, kFwdS2R); }
+void inttmul256_gs_rev2std(int32_t *a) { transform256(a, 0, kInvR2S); }
+void inttmul256_gs_std2rev(int32_t *a) { transform256(a, 0, kInvS2R); }
 
 }  // extern "C"

@@ -198,6 +198,9 @@ int make_plan(uint32_t n, uint64_t q, uint64_t psi, Plan *P, bool cyclic) {
   // standalone inverse NTT: plain n^-1 (ntt256.C:12); pointwise product: R^2 mod q
   tw_pair(P->inv_n, q, bits, &P->fi, &P->fis);
   tw_pair(mulmod(iw[1], P->inv_n, q), q, bits, &P->wfi, &P->wfis);
+  // the reference's unscaled inverses (intt*, inttmul*: intt(ntt(a)) = n a, ntt256.h:16-17)
+  tw_pair(1, q, bits, &P->fu, &P->fus);
+  tw_pair(iw[1], q, bits, &P->wfu, &P->wfus);
   P->r2 = mulmod(r_mod_q, r_mod_q, q);
   return NTTMUL_OK;
 }

@@ -33,6 +33,7 @@ struct Plan {
   int word_bits = 0;                 // 32 when q < 2^31 (lazy [0, 2q) fits a u32), else 64
   uint64_t qinv_neg = 0, f = 0, fs = 0, wf = 0, wfs = 0;
   uint64_t fi = 0, fis = 0, wfi = 0, wfis = 0, r2 = 0;  // standalone inverse / pointwise
+  uint64_t fu = 0, fus = 0, wfu = 0, wfus = 0;          // unscaled inverse (F = 1)
   // interleaved {w, w'} pairs (u32 or u64 each), n entries; entry 0 unused
   std::vector<uint8_t> fw, iw;
 };

@@ -28,6 +28,18 @@ NTTMUL_ERANGE = -5
 NTTMUL_EUNSUPPORTED = -6
 NTTMUL_FLAG_VALIDATE = 1
 NTTMUL_FLAG_CYCLIC = 2
+# transform modes (include/nttmul.h nttmul_transform_*)
+XF_FORWARD = 0
+XF_INVERSE = 1
+XF_STD2REV = 0
+XF_REV2STD = 2
+XF_UNSCALED = 4
+# the reference's n = 256 wrapper set (NTT/ntt256.h:20-69), exported under the same names
+NTT256_WRAPPERS = [
+    "ntt256_ct_rev2std", "ntt256_gs_rev2std", "ntt256_ct_std2rev", "ntt256_gs_std2rev",
+    "intt256_ct_rev2std", "intt256_gs_rev2std", "intt256_ct_std2rev", "intt256_gs_std2rev",
+    "mulntt256_ct_rev2std", "mulntt256_ct_std2rev", "inttmul256_gs_rev2std", "inttmul256_gs_std2rev",
+]
 TABLES = [  # nttmul_table `which` order = the tables of NTT/ntt.h:63-183 (ntt256_tables.h:29-43)
     "psi_powers", "inv_psi_powers", "inv_psi_powers_rev", "scaled_inv_psi_powers",
     "omega_powers", "omega_powers_rev", "inv_omega_powers", "inv_omega_powers_rev",
@@ -108,6 +120,12 @@ def load_library() -> ctypes.CDLL:
     for name in ("ntt256_product1", "ntt256_product4", "ntt_red256_product1", "ntt_red256_product4"):
         getattr(lib, name).argtypes = [vp, vp, vp]
         getattr(lib, name).restype = None
+    for w in ("u32", "u64"):
+        getattr(lib, f"nttmul_transform_batch_{w}").argtypes = [vp, u32, vp, vp, sz]
+    lib.nttmul_transform_device.argtypes = [vp, u32, vp, vp, sz, i32, i32, vp]
+    for name in NTT256_WRAPPERS:
+        getattr(lib, name).argtypes = [vp]
+        getattr(lib, name).restype = None
     _LIB = lib
     return lib
 
@@ -117,7 +135,8 @@ def exported_symbols() -> list:
     import re
     text = open(HEADER_PATH).read()
     return sorted(set(re.findall(r"^\s*(?:const\s+)?(?:int|void|char\s*\*|const char \*)\s*\*?\s*"
-                                 r"(nttmul_\w+|ntt256_\w+|ntt_red256_\w+)\s*\(", text, re.M)))
+                                 r"(nttmul_\w+|i?ntt256_\w+|ntt_red256_\w+|mulntt256_\w+|"
+                                 r"inttmul256_\w+)\s*\(", text, re.M)))
 
 
 def strerror(status: int) -> str:
@@ -212,6 +231,25 @@ class Context:
     def inverse(self, a_hat, dtype=None) -> np.ndarray:
         """Inverse of forward(): nttmul_gs_rev2std (NTT/ntt.C:428) then n^-1."""
         return self._unary("inverse", a_hat, dtype)
+
+    def transform(self, x, mode: int, dtype=None) -> np.ndarray:
+        """nttmul_transform_batch: mode = XF_FORWARD/XF_INVERSE | XF_STD2REV/XF_REV2STD
+        [| XF_UNSCALED] — the reference's wrapper set (NTT/ntt256.h:20-69) for this context."""
+        dtype = dtype or self.io_dtype
+        x = np.ascontiguousarray(x, dtype=dtype)
+        if x.shape[-1] != self.n:
+            raise ValueError("input must have shape [..., n]")
+        out = np.empty_like(x)
+        w = "u32" if dtype == np.uint32 else "u64"
+        fn = getattr(self._lib, f"nttmul_transform_batch_{w}")
+        self._check(fn(self._h, mode, out.ctypes.data, x.ctypes.data, x.size // self.n))
+        return out
+
+    def transform_device(self, out, x, mode: int, batch: int, word_bits: int,
+                         dev: Optional[int] = None, stream: int = 0):
+        dev = self.first_dev if dev is None else dev
+        self._check(self._lib.nttmul_transform_device(self._h, mode, _ptr(out), _ptr(x), batch,
+                                                      word_bits, dev, stream or None))
 
     def pointwise(self, a, b, dtype=None) -> np.ndarray:
         """c[i] = a[i] * b[i] mod q (NTT/ntt.C:131 mul_array)."""
@@ -359,3 +397,14 @@ def ntt_red256_product1(c: np.ndarray, a: np.ndarray, b: np.ndarray) -> None:
 def ntt_red256_product4(c: np.ndarray, a: np.ndarray, b: np.ndarray) -> None:
     """NTT-RED/ntt_red256.C:30."""
     _product256("ntt_red256_product4", c, a, b)
+
+
+def ntt256_transform(name: str, a: np.ndarray) -> None:
+    """One of the reference's n = 256 wrappers (NTT/ntt256.h:20-69, e.g. "ntt256_ct_std2rev",
+    "inttmul256_gs_rev2std") in place on a contiguous int32 array of 256 coefficients."""
+    if name not in NTT256_WRAPPERS:
+        raise ValueError(f"unknown ntt256 wrapper {name}")
+    if not (isinstance(a, np.ndarray) and a.dtype == np.int32 and a.size == 256
+            and a.flags.c_contiguous):
+        raise TypeError("ntt256 wrappers take a contiguous int32 array of 256 coefficients")
+    getattr(load_library(), name)(a.ctypes.data)

@@ -30,6 +30,41 @@ def read_coeffs(path):
     return np.array((vals + [0] * 256)[:256], dtype=np.int64)
 
 
+# NTT/ntt256.h:20-69: wrapper -> (ntt.C loop, ntt256 table it passes)
+WRAPPERS = {
+    "ntt256_ct_rev2std": ("ntt_ct_rev2std", "omega_powers"),
+    "ntt256_gs_rev2std": ("ntt_gs_rev2std", "omega_powers_rev"),
+    "ntt256_ct_std2rev": ("ntt_ct_std2rev", "omega_powers_rev"),
+    "ntt256_gs_std2rev": ("ntt_gs_std2rev", "omega_powers"),
+    "intt256_ct_rev2std": ("ntt_ct_rev2std", "inv_omega_powers"),
+    "intt256_gs_rev2std": ("ntt_gs_rev2std", "inv_omega_powers_rev"),
+    "intt256_ct_std2rev": ("ntt_ct_std2rev", "inv_omega_powers_rev"),
+    "intt256_gs_std2rev": ("ntt_gs_std2rev", "inv_omega_powers"),
+    "mulntt256_ct_rev2std": ("mulntt_ct_rev2std", "mixed_powers"),
+    "mulntt256_ct_std2rev": ("mulntt_ct_std2rev", "mixed_powers_rev"),
+    "inttmul256_gs_rev2std": ("nttmul_gs_rev2std", "inv_mixed_powers_rev"),
+    "inttmul256_gs_std2rev": ("nttmul_gs_std2rev", "inv_mixed_powers"),
+}
+
+
+def wrappers(R):
+    """The twelve n = 256 transform wrappers through the compiled reference's own loops, on 32
+    inputs (one all-(q-1), one all-zero, one unit impulse, the rest random)."""
+    rng = np.random.default_rng(0x57A9)
+    X = rng.integers(0, Q0, (32, 256))
+    X[0] = Q0 - 1; X[1] = 0; X[2] = 0; X[2, 1] = 1
+    P256 = O.Plan(256, Q0, 1002)
+    t = {k: P256.table(k).astype(np.uint16) for k in O.TABLES}
+    out = {"x": X.astype(np.int32)}
+    for name, (fn, tab) in WRAPPERS.items():
+        out[name] = np.array([R.transform(fn, x, t[tab]) for x in X], dtype=np.int32)
+        # the oracle's restatement of the same loop must agree (pins oracle/nttmul_oracle.c)
+        ora = np.array([P256.transform(fn, x.astype(np.uint64), tab) for x in X])
+        assert np.array_equal(ora.astype(np.int64), out[name].astype(np.int64)), name
+    np.savez_compressed(os.path.join(HERE, "ref256_wrappers.npz"), **out)
+    print("ref256_wrappers.npz written")
+
+
 def main():
     if not O.ref_available():
         sys.exit("oracle/_ref/libntt_ref.so missing: run `make -C oracle` with /root/reference present")
@@ -154,8 +189,14 @@ def main():
         sb[key + "_a"] = a; sb[key + "_b"] = b; sb[key + "_c"] = c
         print("schoolbook", key, "done", flush=True)
     np.savez_compressed(os.path.join(HERE, "schoolbook_bigint.npz"), **sb)
+    wrappers(R)
     print("golden fixtures written to", HERE)
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["wrappers"]:
+        if not O.ref_available():
+            sys.exit("oracle/_ref/libntt_ref.so missing")
+        wrappers(O.Ref())
+    else:
+        main()

@@ -334,3 +334,69 @@ def test_host_path_pipeline(n, q, batch, torch_cuda):
     # the standalone transforms take the same path
     fa = ctx.forward(a.astype(dt))
     assert np.array_equal(ctx.inverse(fa).astype(np.uint64), a)
+
+
+# ---------------------------------------------------------------------------------------------
+# The reference's whole transform wrapper set (NTT/ntt256.h:20-69) and its general form
+# ---------------------------------------------------------------------------------------------
+
+def test_ntt256_wrappers_golden(golden_dir, torch_cuda):
+    """The twelve exported ntt256 wrappers equal the compiled reference's, in place, on the
+    fixture's 32 inputs (edge rows: all q-1, all 0, unit impulse)."""
+    g = np.load(os.path.join(golden_dir, "ref256_wrappers.npz"))
+    for name in nttmul.NTT256_WRAPPERS:
+        for x, exp in zip(g["x"], g[name]):
+            a = np.ascontiguousarray(x, dtype=np.int32)
+            nttmul.ntt256_transform(name, a)
+            assert np.array_equal(a, exp), name
+
+
+def _xf_expected(P, x, mode, cyclic, n, q):
+    inv, rev = mode & nttmul.XF_INVERSE, mode & nttmul.XF_REV2STD
+    if not inv:
+        fn, tab = ((("ntt_ct_rev2std", "omega_powers") if rev else ("ntt_ct_std2rev", "omega_powers_rev"))
+                   if cyclic else
+                   (("mulntt_ct_rev2std", "mixed_powers") if rev else ("mulntt_ct_std2rev", "mixed_powers_rev")))
+    else:
+        fn, tab = ((("ntt_gs_rev2std", "inv_omega_powers_rev") if rev else ("ntt_gs_std2rev", "inv_omega_powers"))
+                   if cyclic else
+                   (("nttmul_gs_rev2std", "inv_mixed_powers_rev") if rev else ("nttmul_gs_std2rev", "inv_mixed_powers")))
+    y = P.transform(fn, x, tab)
+    if inv and not (mode & nttmul.XF_UNSCALED):
+        inv_n = pow(n, q - 2, q)
+        y = np.array([int(v) * inv_n % q for v in y], dtype=np.uint64)
+    return y
+
+
+@pytest.mark.parametrize("cyclic", [False, True])
+@pytest.mark.parametrize("n,q", [(256, Q30), (1024, Q31), (4096, Q31), (4096, Q62), (8192, Q30),
+                                 (65536, Q62)])
+def test_transform_modes_vs_oracle(n, q, cyclic, torch_cuda):
+    """nttmul_transform_*: every (direction, order, scaling) equals the reference's loop of the
+    same name (restated in the oracle; pinned by test_oracle.py::test_wrappers_golden)."""
+    P = O.Plan(n, q)
+    ctx = _ctx(n, q, psi=P.omega if cyclic else 0, cyclic=cyclic)  # same omega = psi^2
+    x, _ = O.fill_inputs(n, q, 21, 2)
+    x[1, :] = q - 1
+    dt = np.uint32 if q < (1 << 32) else np.uint64
+    for mode in (0, 2, 1, 3, 1 | 4, 3 | 4):
+        got = ctx.transform(x.astype(dt), mode).astype(np.uint64)
+        for i in range(2):
+            assert np.array_equal(got[i], _xf_expected(P, x[i], mode, cyclic, n, q)), (mode, i)
+
+
+def test_transform_modes_device(torch_cuda):
+    torch = torch_cuda
+    n, q, batch = 4096, Q31, 1024
+    ctx = _ctx(n, q)
+    a = torch.empty(batch * n, dtype=torch.int32, device="cuda")
+    b = torch.empty_like(a)
+    s = torch.cuda.current_stream().cuda_stream
+    ctx.fill_random_device(a, b, 0, batch, 32, stream=s)
+    f, back = torch.empty_like(a), torch.empty_like(a)
+    for fwd, inv in ((nttmul.XF_REV2STD, nttmul.XF_INVERSE | nttmul.XF_STD2REV),
+                     (nttmul.XF_STD2REV, nttmul.XF_INVERSE | nttmul.XF_REV2STD)):
+        ctx.transform_device(f, a, fwd, batch, 32, stream=s)
+        ctx.transform_device(back, f, inv, batch, 32, stream=s)
+        torch.cuda.synchronize()
+        assert torch.equal(back, a)

@@ -112,6 +112,55 @@ def test_transforms_match_reference():
                                       P.transform(name, a, tab).astype(np.int32)), (n, name)
 
 
+WRAPPERS = {  # NTT/ntt256.h:20-69: wrapper -> (ntt.C loop, ntt256 table)
+    "ntt256_ct_rev2std": ("ntt_ct_rev2std", "omega_powers"),
+    "ntt256_gs_rev2std": ("ntt_gs_rev2std", "omega_powers_rev"),
+    "ntt256_ct_std2rev": ("ntt_ct_std2rev", "omega_powers_rev"),
+    "ntt256_gs_std2rev": ("ntt_gs_std2rev", "omega_powers"),
+    "intt256_ct_rev2std": ("ntt_ct_rev2std", "inv_omega_powers"),
+    "intt256_gs_rev2std": ("ntt_gs_rev2std", "inv_omega_powers_rev"),
+    "intt256_ct_std2rev": ("ntt_ct_std2rev", "inv_omega_powers_rev"),
+    "intt256_gs_std2rev": ("ntt_gs_std2rev", "inv_omega_powers"),
+    "mulntt256_ct_rev2std": ("mulntt_ct_rev2std", "mixed_powers"),
+    "mulntt256_ct_std2rev": ("mulntt_ct_std2rev", "mixed_powers_rev"),
+    "inttmul256_gs_rev2std": ("nttmul_gs_rev2std", "inv_mixed_powers_rev"),
+    "inttmul256_gs_std2rev": ("nttmul_gs_std2rev", "inv_mixed_powers"),
+}
+
+
+def test_wrappers_golden(golden_dir):
+    """The oracle's loops reproduce the compiled reference's twelve ntt256 wrappers
+    (tests/golden/ref256_wrappers.npz) on all 32 fixture inputs."""
+    g = np.load(os.path.join(golden_dir, "ref256_wrappers.npz"))
+    P = O.Plan(256, Q0, 1002)
+    for name, (fn, tab) in WRAPPERS.items():
+        for x, exp in zip(g["x"], g[name]):
+            got = P.transform(fn, x.astype(np.uint64), tab)
+            assert np.array_equal(got, exp.astype(np.uint64)), name
+
+
+def _bitrev_perm(v):
+    b = int(np.log2(len(v)))
+    return v[[int(format(i, f"0{b}b")[::-1], 2) for i in range(len(v))]]
+
+
+def test_order_identities():
+    """rev2std = P o std2rev o P (P = bit reversal) for every loop pair, and CT == GS per order:
+    what lets the library run every wrapper with its two transform kernels."""
+    rng = np.random.default_rng(3)
+    for n, q in ((256, Q0), (1024, 2013265921), (4096, 2013265921)):
+        P = O.Plan(n, q)
+        x = rng.integers(0, q, n).astype(np.uint64)
+        T = P.transform
+        for fwd, rev in ((("mulntt_ct_std2rev", "mixed_powers_rev"), ("mulntt_ct_rev2std", "mixed_powers")),
+                         (("ntt_ct_std2rev", "omega_powers_rev"), ("ntt_ct_rev2std", "omega_powers")),
+                         (("nttmul_gs_rev2std", "inv_mixed_powers_rev"), ("nttmul_gs_std2rev", "inv_mixed_powers")),
+                         (("ntt_gs_rev2std", "inv_omega_powers_rev"), ("ntt_gs_std2rev", "inv_omega_powers"))):
+            assert np.array_equal(T(rev[0], x, rev[1]), _bitrev_perm(T(fwd[0], _bitrev_perm(x), fwd[1])))
+        assert np.array_equal(T("ntt_gs_std2rev", x, "omega_powers"), T("ntt_ct_std2rev", x, "omega_powers_rev"))
+        assert np.array_equal(T("ntt_gs_rev2std", x, "omega_powers_rev"), T("ntt_ct_rev2std", x, "omega_powers"))
+
+
 @needs_ref
 def test_random_products_match_reference():
     R = O.Ref()
