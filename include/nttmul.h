@@ -63,7 +63,7 @@ typedef struct {
 typedef struct {
   uint32_t n, logn;
   uint64_t q, psi, omega, inv_psi, inv_omega, inv_n;
-  uint32_t word_bits;  /* 32: lazy 32-bit Shoup kernels (q < 2^31); 64: 64-bit kernels          */
+  uint32_t word_bits;  /* 32: 32-bit kernels (q < 2^32); 64: 64-bit kernels (q < 2^62)           */
   int ndev;
   int kernel;          /* 1 = fused single-launch polymult, 2 = multi-pass (n > 4096)             */
   uint32_t cyclic;     /* 1 with NTTMUL_FLAG_CYCLIC (psi, inv_psi are 0 then)                    */

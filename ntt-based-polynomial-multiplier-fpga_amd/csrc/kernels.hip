@@ -575,6 +575,13 @@ hipError_t launch_polymul(const LaunchTables &T, const void *a, const void *b, v
     return big ? multipass<Arith32H, uint32_t>(T, a, b, c, batch, scr, s)
                : fused<Arith32H, uint32_t>(T, a, b, c, batch, s);
   }
+  if (T.word_bits == 32 && T.q >= (1ull << 31)) {  // full 32-bit modulus
+    if (io_bits == 64)
+      return big ? multipass<Arith32W, uint64_t>(T, a, b, c, batch, scr, s)
+                 : fused<Arith32W, uint64_t>(T, a, b, c, batch, s);
+    return big ? multipass<Arith32W, uint32_t>(T, a, b, c, batch, scr, s)
+               : fused<Arith32W, uint32_t>(T, a, b, c, batch, s);
+  }
   if (T.word_bits == 32) {
     if (io_bits == 64)  // 64-bit storage of a q < 2^31 product: same 32-bit arithmetic
       return big ? multipass<Arith32, uint64_t>(T, a, b, c, batch, scr, s)
@@ -665,6 +672,9 @@ static hipError_t launch_xform_dir(const LaunchTables &T, const void *in, void *
   if (NTTMUL_A32H && T.word_bits == 32 && T.q < (1ull << 30))
     return io_bits == 64 ? xform_any<Arith32H, uint64_t, DIR>(T, in, out, batch, scr, s)
                          : xform_any<Arith32H, uint32_t, DIR>(T, in, out, batch, scr, s);
+  if (T.word_bits == 32 && T.q >= (1ull << 31))
+    return io_bits == 64 ? xform_any<Arith32W, uint64_t, DIR>(T, in, out, batch, scr, s)
+                         : xform_any<Arith32W, uint32_t, DIR>(T, in, out, batch, scr, s);
   if (T.word_bits == 32)
     return io_bits == 64 ? xform_any<Arith32, uint64_t, DIR>(T, in, out, batch, scr, s)
                          : xform_any<Arith32, uint32_t, DIR>(T, in, out, batch, scr, s);
@@ -693,6 +703,9 @@ hipError_t launch_pointwise(const LaunchTables &T, const void *a, const void *b,
                             size_t batch, int io_bits, hipStream_t s) {
   const size_t total = batch << T.logn;
   if (!total) return hipSuccess;
+  if (T.word_bits == 32 && T.q >= (1ull << 31))
+    return io_bits == 64 ? pointwise<Arith32W, uint64_t>(T, a, b, c, total, s)
+                         : pointwise<Arith32W, uint32_t>(T, a, b, c, total, s);
   if (T.word_bits == 32)
     return io_bits == 64 ? pointwise<Arith32, uint64_t>(T, a, b, c, total, s)
                          : pointwise<Arith32, uint32_t>(T, a, b, c, total, s);

@@ -9,7 +9,7 @@ namespace nttmul {
 // Per-device view of a plan: what a launch needs (pointers are device memory).
 struct LaunchTables {
   uint32_t logn;
-  int word_bits;           // 32 -> Arith32 (q < 2^31), 64 -> Arith64
+  int word_bits;           // 32 -> Arith32H / Arith32 / Arith32W by q (q < 2^32), 64 -> Arith64
   uint64_t q, qinv_neg;    // -q^-1 mod 2^word_bits
   uint64_t f, fs, wf, wfs; // F = n^-1 R mod q and iw[1] F, as (value, companion) pairs
   uint64_t fi, fis, wfi, wfis; // n^-1 and iw[1] n^-1 (standalone inverse), with companions

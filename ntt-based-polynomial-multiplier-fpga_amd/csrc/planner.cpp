@@ -76,8 +76,8 @@ static uint64_t companion(uint64_t w, uint64_t q, int bits) {
 // (value, companion) pair the device multiplies by: Shoup (w, floor(w 2^bits / q)), or for
 // Arith32 with NTTMUL_A32_MONT the Montgomery form (w 2^32 mod q, that times -q^-1 mod 2^32)
 static void tw_pair(uint64_t w, uint64_t q, int bits, uint64_t *v, uint64_t *c) {
-#if NTTMUL_A32_MONT
-  if (bits == 32) {
+  // Arith32W (q >= 2^31) always takes the Montgomery form
+  if (bits == 32 && (NTTMUL_A32_MONT || q >= (1ull << 31))) {
     uint64_t inv = q;
     for (int i = 0; i < 5; i++) inv *= 2 - q * inv;
     const uint64_t w1 = (uint64_t)(((u128)w << 32) % q);
@@ -85,7 +85,6 @@ static void tw_pair(uint64_t w, uint64_t q, int bits, uint64_t *v, uint64_t *c) 
     *c = (w1 * (0 - inv)) & 0xFFFFFFFFull;
     return;
   }
-#endif
   *v = w;
   *c = companion(w, q, bits);
 }
@@ -142,7 +141,7 @@ int make_plan(uint32_t n, uint64_t q, uint64_t psi, Plan *P, bool cyclic) {
   P->inv_psi = cyclic ? 0 : powmod(psi, q - 2, q);
   P->inv_omega = powmod(P->omega, q - 2, q);
   P->inv_n = powmod(n, q - 2, q);
-  P->word_bits = q < (1ull << 31) ? 32 : 64;
+  P->word_bits = q < (1ull << 32) ? 32 : 64;  // 32: Arith32H / Arith32 / Arith32W by q
   const int bits = P->word_bits;
 
   std::vector<uint64_t> fw(n, 0), iw(n, 0);

@@ -30,7 +30,7 @@ struct Plan {
   bool cyclic = false;               // x^n - 1 (FPGA-compat) instead of x^n + 1
   uint32_t n = 0, logn = 0;
   uint64_t q = 0, psi = 0, omega = 0, inv_psi = 0, inv_omega = 0, inv_n = 0;
-  int word_bits = 0;                 // 32 when q < 2^31 (lazy [0, 2q) fits a u32), else 64
+  int word_bits = 0;                 // 32 when q < 2^32 (table words, kernel family), else 64
   uint64_t qinv_neg = 0, f = 0, fs = 0, wf = 0, wfs = 0;
   uint64_t fi = 0, fis = 0, wfi = 0, wfis = 0, r2 = 0;  // standalone inverse / pointwise
   uint64_t fu = 0, fus = 0, wfu = 0, wfus = 0;          // unscaled inverse (F = 1)

@@ -122,7 +122,7 @@ def test_random_vs_oracle(n, q, torch_cuda):
 
 
 @pytest.mark.parametrize("n", [8192, 16384, 32768, 65536])
-@pytest.mark.parametrize("q", [Q31, Q30, Q62])
+@pytest.mark.parametrize("q", [Q31, Q30, Q32, Q62])
 def test_multipass_vs_oracle(n, q, torch_cuda):
     """n > 4096: column pass + fused rows + inverse column pass."""
     P = O.Plan(n, q)
@@ -229,7 +229,7 @@ def test_transforms_ref256_golden(golden_dir, torch_cuda):
 
 
 @pytest.mark.parametrize("n", [256, 1024, 4096, 8192, 65536])
-@pytest.mark.parametrize("q", [Q31, Q30, Q62])
+@pytest.mark.parametrize("q", [Q31, Q30, Q32, Q62])
 def test_transforms_vs_oracle(n, q, torch_cuda):
     P = O.Plan(n, q)
     ctx = _ctx(n, q)
@@ -369,8 +369,8 @@ def _xf_expected(P, x, mode, cyclic, n, q):
 
 
 @pytest.mark.parametrize("cyclic", [False, True])
-@pytest.mark.parametrize("n,q", [(256, Q30), (1024, Q31), (4096, Q31), (4096, Q62), (8192, Q30),
-                                 (65536, Q62)])
+@pytest.mark.parametrize("n,q", [(256, Q30), (1024, Q31), (4096, Q31), (4096, Q32), (4096, Q62),
+                                 (8192, Q30), (16384, Q32), (65536, Q62)])
 def test_transform_modes_vs_oracle(n, q, cyclic, torch_cuda):
     """nttmul_transform_*: every (direction, order, scaling) equals the reference's loop of the
     same name (restated in the oracle; pinned by test_oracle.py::test_wrappers_golden)."""
