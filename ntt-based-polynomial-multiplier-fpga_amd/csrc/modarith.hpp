@@ -208,15 +208,31 @@ struct Arith32W {
 #ifndef NTTMUL_A64_PLAIN
 #define NTTMUL_A64_PLAIN 0
 #endif
+// borrow-chain csub and mov-lean high product (tools/kbench A/B)
+#ifndef NTTMUL_A64_V2
+#define NTTMUL_A64_V2 1
+#endif
 struct Arith64 {
   using word = uint64_t;
   static constexpr int kBits = 64;
   uint64_t q;
   uint64_t qinv_neg;  // -q^-1 mod 2^64
 
+  // x in [0, 2m) -> [0, m).  Spelled as a 32-bit borrow chain so the select uses the borrow of
+  // v_subb_co_u32 directly (the 64-bit __builtin_sub_overflow form adds a v_cmp_gt_u64).
   __device__ __forceinline__ static uint64_t csub(uint64_t x, uint64_t m) {
+#if NTTMUL_A64_V2
+    const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
+    const uint32_t ml = (uint32_t)m, mh = (uint32_t)(m >> 32);
+    uint32_t lo, t, hi;
+    const bool b1 = __builtin_sub_overflow(xl, ml, &lo);
+    const bool b2 = __builtin_sub_overflow(xh, mh, &t);
+    const bool b3 = __builtin_sub_overflow(t, (uint32_t)b1, &hi);
+    return (b2 | b3) ? x : (((uint64_t)hi << 32) | lo);
+#else
     uint64_t d;
     return __builtin_sub_overflow(x, m, &d) ? x : d;
+#endif
   }
   // high 64 bits of the 128-bit product x * s, from four 32x32 products
   __device__ __forceinline__ static uint64_t mulhi64(uint64_t x, uint64_t s) {
@@ -225,9 +241,16 @@ struct Arith64 {
 #else
     const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
     const uint32_t sl = (uint32_t)s, sh = (uint32_t)(s >> 32);
+#if NTTMUL_A64_V2
+    const uint64_t p00 = (uint64_t)xl * sl;
+    const uint64_t t = (uint64_t)xl * sh + (p00 >> 32);
+    const uint64_t u = (uint64_t)xh * sl + (t & 0xFFFFFFFFull);
+    return (uint64_t)xh * sh + (t >> 32) + (u >> 32);
+#else
     const uint64_t t = (uint64_t)xl * sh + __umulhi(xl, sl);
     const uint64_t u = (uint64_t)xh * sl + (uint32_t)t;
     return (uint64_t)xh * sh + ((t >> 32) + (u >> 32));
+#endif
 #endif
   }
   // low 64 bits of x * w
@@ -245,7 +268,20 @@ struct Arith64 {
   // x * w mod q in [0, 2q) for any 64-bit x (Shoup, w' = floor(w 2^64 / q))
   __device__ __forceinline__ uint64_t shoup(uint64_t x, uint64_t w, uint64_t ws) const {
     const uint64_t qh = mulhi64(x, ws);
+#if NTTMUL_A64_V2
+    // lo64(x w) - lo64(qh q) in one pass: D = xl wl + hl (2^32 - ql) carries the low word and a
+    // high word off by +hl, which the complemented constants absorb (2 v_mad_u64_u32,
+    // 4 v_mul_lo_u32, 2 v_add3_u32; no 64-bit subtract chain)
+    const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
+    const uint32_t wl = (uint32_t)w, wh = (uint32_t)(w >> 32);
+    const uint32_t hl = (uint32_t)qh, hh = (uint32_t)(qh >> 32);
+    const uint32_t nql = 0u - (uint32_t)q, nqh1 = ~(uint32_t)(q >> 32);
+    const uint64_t D = (uint64_t)xl * wl + (uint64_t)hl * nql;
+    const uint32_t hi = (uint32_t)(D >> 32) + xl * wh + xh * wl + hl * nqh1 + hh * nql;
+    return ((uint64_t)hi << 32) | (uint32_t)D;
+#else
     return mullo64(x, w) - mullo64(qh, q);
+#endif
   }
 #if NTTMUL_A64_PLAIN
   static constexpr uint64_t kLazy = 2;  // values in [0, 2q)
