@@ -97,10 +97,18 @@ def cpu_baseline(n: int, q: int, target_s: float):
     for _ in range(reps):
         _, t = P.fast_batch_u32(a, b, threads)
         total_t += t
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
     return {"value": per * reps / total_t, "unit": "polymults/s", "cores": threads, "kind": "port",
             "sample": f"{per * reps} polymults (n={n}, q={q}) = {reps} passes over {per} "
-                      f"counter-based inputs, OpenMP {threads} threads, "
-                      f"{total_t:.1f} s, oracle/nttmul_oracle.c orc_fast_batch_u32"}
+                      f"counter-based inputs, OpenMP {threads} threads of {os.cpu_count()} "
+                      f"({model}), {total_t:.1f} s, oracle/nttmul_oracle.c orc_fast_batch_u32"}
 
 
 def host_io(ctx, a_dev, b_dev, batch: int, n: int, wb: int, reps: int = 3):
