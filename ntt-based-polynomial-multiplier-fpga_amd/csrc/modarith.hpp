@@ -123,11 +123,11 @@ struct Arith32T {
     X = shoup(x + y, f, fs);
     Y = shoup(x - y + q, wf, wfs);
   }
-  // Montgomery product a b 2^-32 mod q, inputs lazy (H: < 4q, else < 2q), output in [0, 2q):
-  // both reduced below 2q first, t + m q < 4 q^2 + 2^32 q < 2^64.
+  // Montgomery product a b 2^-32 mod q, inputs lazy (H: < 4q, else < 2q), output in [0, 2q).
+  // H: both reduced below 2q, t + m q < 4 q^2 + 2^32 q < 2^64.  Otherwise only a is reduced
+  // (below q): a b + m q < 2 q^2 + 2^32 q < 2^64 and (a b + m q) / 2^32 < q (2q / 2^32 + 1) < 2q.
   __device__ __forceinline__ uint32_t mont(uint32_t a, uint32_t b) const {
-    const uint32_t m2 = H ? 2 * q : q;
-    const uint32_t ar = H ? csub(a, m2) : csub(a, q), br = H ? csub(b, m2) : csub(b, q);
+    const uint32_t ar = H ? csub(a, 2 * q) : csub(a, q), br = H ? csub(b, 2 * q) : b;
     uint64_t t = (uint64_t)ar * br;
     uint32_t m = (uint32_t)t * qinv_neg;
     uint64_t u = t + (uint64_t)m * q;
