@@ -218,8 +218,12 @@ class CopyPool {
 
  private:
   CopyPool() {
+    // NTTMUL_COPY_THREADS (default 8, at most the host's hardware threads) staging threads
     unsigned hw = std::thread::hardware_concurrency();
-    workers_ = hw > 1 ? std::min(hw - 1, 7u) : 0;
+    unsigned want = 8;
+    if (const char *e = getenv("NTTMUL_COPY_THREADS")) want = (unsigned)std::max(1, atoi(e));
+    want = std::min(want, std::max(hw, 1u));
+    workers_ = want - 1;
     for (unsigned i = 0; i < workers_; i++) std::thread([this, i] { run(i); }).detach();
   }
   void run(unsigned i) {
