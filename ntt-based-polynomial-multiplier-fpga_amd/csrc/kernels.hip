@@ -36,6 +36,11 @@
 #ifndef NTTMUL_A32H
 #define NTTMUL_A32H 1
 #endif
+// incomplete transforms in the product kernel: the last D = A::kBaseD stages become base
+// multiplications of 2^D-coefficient blocks (0: full transforms + pointwise Montgomery product)
+#ifndef NTTMUL_BASE_D
+#define NTTMUL_BASE_D 1
+#endif
 // skip the reduction of X in the first forward stage (input canonical by contract)
 #ifndef NTTMUL_FIRST_XC
 #define NTTMUL_FIRST_XC 1
@@ -110,6 +115,12 @@ struct Groups {
     if (lr >= lns) return (j << lns) >> lr;
     return (j << (lns - lr)) + (sidx >> lr);
   }
+  // register holding element offset o in group g's layout (inverse of off)
+  static constexpr int reg_of(int g, int o) {
+    for (int k = 0; k < 16; k++)
+      if (off(g, k) == o) return k;
+    return -1;
+  }
   static constexpr int pad(int e) { return e + (e >> 4); }
   static constexpr int NP = N + N / 16;  // padded LDS words per polynomial
 };
@@ -135,16 +146,19 @@ __device__ __forceinline__ void st_stream(T *p, T v) {
 #endif
 }
 
-// Forward CT stages of group g on NPOLY (1 or 2) polynomials (same twiddles).
-template <class A, int LOGS, int g, int NPOLY = 2>
+// Forward CT stages of group g on NPOLY (1 or 2) polynomials (same twiddles).  SKIP: leave out
+// the last SKIP stages of the group (the incomplete transform of the product kernel, see
+// base_mult); the twiddles of the last stage performed are kept in zw[X register].
+template <class A, int LOGS, int g, int NPOLY = 2, int SKIP = 0>
 __device__ __forceinline__ void fwd_group(const A &ar, typename A::word (&x)[16],
                                           typename A::word (&y)[16],
                                           const TwPair<typename A::word> *__restrict__ tw, int j,
-                                          int row, int l1) {
+                                          int row, int l1,
+                                          TwPair<typename A::word> (&zw)[16]) {
   using Gr = Groups<LOGS>;
   constexpr int S = Gr::S(g), st0 = Gr::ST0(g), ns = Gr::NS(g);
 #pragma unroll
-  for (int l = 0; l < S; l++) {
+  for (int l = 0; l < S - SKIP; l++) {
     const int dist = 8 >> l;
     const int st = st0 + l;
     const int tbase = (1 << (l1 + st)) + (row << st);
@@ -154,6 +168,7 @@ __device__ __forceinline__ void fwd_group(const A &ar, typename A::word (&x)[16]
       const int m = k / ns;
       const int idx = tbase + (Gr::blk(g, j, k) << l) + (m >> (S - l));
       const TwPair<typename A::word> t = tw[NTTMUL_ABL_TWMASK ? (idx & NTTMUL_ABL_TWMASK) : idx];
+      if (l == S - SKIP - 1) zw[k] = t;
       // global stage 0 of a whole polynomial reads canonical input (the API contract, [0, q)):
       // its X operands need no reduction
       if (NTTMUL_FIRST_XC && g == 0 && l == 0 && l1 == 0) {
@@ -168,14 +183,15 @@ __device__ __forceinline__ void fwd_group(const A &ar, typename A::word (&x)[16]
 }
 
 // Inverse GS stages of group g (reverse stage order).  SCALE: fold F into the global stage 0.
-template <class A, int LOGS, int g, bool SCALE>
+// SKIP: leave out the group's last SKIP forward stages (the first SKIP inverse ones).
+template <class A, int LOGS, int g, bool SCALE, int SKIP = 0>
 __device__ __forceinline__ void inv_group(const KParams<A> &P, typename A::word (&x)[16],
                                           const TwPair<typename A::word> *__restrict__ tw, int j,
                                           int row, int l1) {
   using Gr = Groups<LOGS>;
   constexpr int S = Gr::S(g), st0 = Gr::ST0(g), ns = Gr::NS(g);
 #pragma unroll
-  for (int l = S - 1; l >= 0; l--) {
+  for (int l = S - 1 - SKIP; l >= 0; l--) {
     const int dist = 8 >> l;
     const int st = st0 + l;
     const int tbase = (1 << (l1 + st)) + (row << st);
@@ -232,30 +248,72 @@ __device__ __forceinline__ void exchange(W (&x)[16], W (&y)[16], W *lds_x, W *ld
   __syncthreads();
 }
 
-template <class A, int LOGS, int g, int NPOLY = 2>
+template <class A, int LOGS, int g, int NPOLY = 2, int SKIP = 0>
 __device__ __forceinline__ void fwd_all(const A &ar, typename A::word (&x)[16],
                                         typename A::word (&y)[16], typename A::word *lx,
                                         typename A::word *ly,
                                         const TwPair<typename A::word> *__restrict__ tw, int j,
-                                        int row, int l1) {
+                                        int row, int l1, TwPair<typename A::word> (&zw)[16]) {
   using Gr = Groups<LOGS>;
-  fwd_group<A, LOGS, g, NPOLY>(ar, x, y, tw, j, row, l1);
-  if constexpr (g + 1 < Gr::G) {
+  constexpr bool last = g + 1 == Gr::G;
+  fwd_group<A, LOGS, g, NPOLY, last ? SKIP : 0>(ar, x, y, tw, j, row, l1, zw);
+  if constexpr (!last) {
     exchange<LOGS, g, g + 1, NPOLY>(x, y, lx, ly, j);
-    fwd_all<A, LOGS, g + 1, NPOLY>(ar, x, y, lx, ly, tw, j, row, l1);
+    fwd_all<A, LOGS, g + 1, NPOLY, SKIP>(ar, x, y, lx, ly, tw, j, row, l1, zw);
   }
 }
 
-template <class A, int LOGS, int g, bool SCALE>
+template <class A, int LOGS, int g, bool SCALE, int SKIP = 0>
 __device__ __forceinline__ void inv_all(const KParams<A> &P, typename A::word (&x)[16],
                                         typename A::word (&y)[16], typename A::word *lx,
                                         typename A::word *ly,
                                         const TwPair<typename A::word> *__restrict__ tw, int j,
                                         int row, int l1) {
-  inv_group<A, LOGS, g, SCALE>(P, x, tw, j, row, l1);
+  using Gr = Groups<LOGS>;
+  inv_group<A, LOGS, g, SCALE, g + 1 == Gr::G ? SKIP : 0>(P, x, tw, j, row, l1);
   if constexpr (g > 0) {
     exchange<LOGS, g, g - 1, 1>(x, y, lx, ly, j);
-    inv_all<A, LOGS, g - 1, SCALE>(P, x, y, lx, ly, tw, j, row, l1);
+    inv_all<A, LOGS, g - 1, SCALE, SKIP>(P, x, y, lx, ly, tw, j, row, l1);
+  }
+}
+
+// Incomplete-transform product (Kyber-style): the last D forward stages, the pointwise product
+// and the first D inverse stages are replaced by products in Z_q[x]/(x^(2^D) - z) of the 2^D-
+// coefficient blocks the truncated forward transform leaves.  The CT butterfly with twiddle w
+// splits x^(2d) - w^2 into (x^d - w)(x^d + w), so a block that was the X (Y) output of the last
+// performed stage is a residue mod x^(2^D) - w (x^(2^D) + w): z = +-w, the twiddle already in
+// zw.  The last group always starts at a multiple of 16 elements, so bit D of a register's
+// offset says X or Y.  Same canonical output as the full transform (the product is unique).
+template <class A, int LOGS, int D>
+__device__ __forceinline__ void base_mult(const A &ar, typename A::word (&x)[16],
+                                          const typename A::word (&y)[16],
+                                          const TwPair<typename A::word> (&zw)[16]) {
+  using Gr = Groups<LOGS>;
+  constexpr int g = Gr::G - 1, B = 1 << D;
+  static_assert(D == 0 || Gr::S(g) > D, "last register group too short for the base blocks");
+  if constexpr (D == 0) {
+#pragma unroll
+    for (int k = 0; k < 16; k++) x[k] = ar.mont(x[k], y[k]);
+  } else {
+#pragma unroll
+    for (int k0 = 0; k0 < 16; k0++) {
+      const int o0 = Gr::off(g, k0);
+      if (o0 & (B - 1)) continue;  // k0 holds a block's constant coefficient
+      int r[B];
+#pragma unroll
+      for (int i = 0; i < B; i++) r[i] = Gr::reg_of(g, o0 + i);
+      const bool neg = (o0 >> D) & 1;
+      const TwPair<typename A::word> z = zw[Gr::reg_of(g, o0 & ~B)];
+      typename A::word a[B], b[B];
+#pragma unroll
+      for (int i = 0; i < B; i++) a[i] = x[r[i]], b[i] = y[r[i]];
+      if (neg)
+        ar.template basemul<B, true>(a, b, z.w, z.ws);
+      else
+        ar.template basemul<B, false>(a, b, z.w, z.ws);
+#pragma unroll
+      for (int i = 0; i < B; i++) x[r[i]] = a[i];
+    }
   }
 }
 
@@ -296,10 +354,11 @@ __global__ __launch_bounds__(256, NTTMUL_MIN_WAVES) void k_rows(KParams<A> P, co
   }
 #endif
   W *lx = lds[pb][0], *ly = lds[pb][NTTMUL_LDS_REGIONS - 1];
-  fwd_all<A, LOGS, 0>(P.ar, x, y, lx, ly, P.fw, j, row, L1);
-#pragma unroll
-  for (int k = 0; k < 16; k++) x[k] = P.ar.mont(x[k], y[k]);
-  inv_all<A, LOGS, G - 1, L1 == 0>(P, x, y, lx, ly, P.iw, j, row, L1);
+  constexpr int D = NTTMUL_BASE_D ? A::kBaseD : 0;
+  TwPair<W> zw[16];
+  fwd_all<A, LOGS, 0, 2, D>(P.ar, x, y, lx, ly, P.fw, j, row, L1, zw);
+  base_mult<A, LOGS, D>(P.ar, x, y, zw);
+  inv_all<A, LOGS, G - 1, L1 == 0, D>(P, x, y, lx, ly, P.iw, j, row, L1);
 #if NTTMUL_ABL_NOSTORE
   W acc = 0;
 #pragma unroll
@@ -340,8 +399,9 @@ __global__ __launch_bounds__(256) void k_xform(KParams<A> P, const TIn *__restri
   W x[16], y[16];
 #pragma unroll
   for (int k = 0; k < 16; k++) x[k] = to_word<W>(in[base_in + Gr::off(GIN, k)]);
+  TwPair<W> zw[16];
   if (DIR == 0)
-    fwd_all<A, LOGS, 0, 1>(P.ar, x, y, lds[pb], lds[pb], P.fw, j, row, L1);
+    fwd_all<A, LOGS, 0, 1>(P.ar, x, y, lds[pb], lds[pb], P.fw, j, row, L1, zw);
   else
     inv_all<A, LOGS, G - 1, L1 == 0>(P, x, y, lds[pb], lds[pb], P.iw, j, row, L1);
   if (live) {
@@ -507,6 +567,19 @@ static KParams<A> make_params(const LaunchTables &T) {
   return P;
 }
 
+// KParams for the product kernels: with incomplete transforms the inverse skips D stages and
+// leaves (n / 2^D) c, so the folded scale is F 2^D
+template <class A>
+static KParams<A> product_params(const LaunchTables &T) {
+  using W = typename A::word;
+  KParams<A> P = make_params<A>(T);
+  static_assert(A::kBaseD == 0 || A::kBaseD == 2, "planner provides F 2^D for D = 2 only");
+  if (NTTMUL_BASE_D && A::kBaseD == 2) {
+    P.f = (W)T.f4; P.fs = (W)T.f4s; P.wf = (W)T.wf4; P.wfs = (W)T.wf4s;
+  }
+  return P;
+}
+
 template <class A, class TIn, class TOut, int LOGS, int L1>
 static hipError_t launch_rows(const KParams<A> &P, const void *a, const void *b, void *c,
                               size_t units, hipStream_t s) {
@@ -522,7 +595,7 @@ static hipError_t launch_rows(const KParams<A> &P, const void *a, const void *b,
 template <class A, class IO>
 static hipError_t fused(const LaunchTables &T, const void *a, const void *b, void *c,
                         size_t batch, hipStream_t s) {
-  const KParams<A> P = make_params<A>(T);
+  const KParams<A> P = product_params<A>(T);
   switch (T.logn) {
     case 8: return launch_rows<A, IO, IO, 8, 0>(P, a, b, c, batch, s);
     case 9: return launch_rows<A, IO, IO, 9, 0>(P, a, b, c, batch, s);
@@ -538,7 +611,7 @@ template <class A, class IO, int L1>
 static hipError_t multipass_l1(const LaunchTables &T, const void *a, const void *b, void *c,
                                size_t batch, void *ta, void *tb, void *tc, hipStream_t s) {
   using W = typename A::word;
-  const KParams<A> P = make_params<A>(T);
+  const KParams<A> P = product_params<A>(T);
   constexpr int LOGS = 12;
   const size_t cols = batch << LOGS;
   const unsigned cblocks = (unsigned)((cols + 255) / 256);

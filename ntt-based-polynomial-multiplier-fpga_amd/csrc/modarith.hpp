@@ -137,6 +137,51 @@ struct Arith32T {
   __device__ __forceinline__ uint32_t canon(uint32_t x) const {
     return H ? csub(csub(x, 2 * q), q) : csub(x, q);
   }
+
+  // Base multiplication of the incomplete transform (kernels.hip base_mult): a = a b 2^-32 in
+  // Z_q[x]/(x^B - z), z = (NEG ? -1 : 1) w for the Montgomery-form twiddle (w1, w2).  Inputs
+  // lazy (forward-transform bounds), output in [0, 2q) like mont().  Schoolbook over 64-bit
+  // accumulators, one Montgomery reduction per output coefficient; the wrapped terms use
+  // b'_i = z b_i (one twiddle product each).
+  //   q < 2^31: a, b, b' canonical, each sum < B q^2 < 2^64 (B = 4); the Montgomery sum can
+  //             reach 2^65, its carry is folded into the final conditional subtraction.
+  //   H       : a < 2q, b and b' canonical, sum < 2 B q^2 < 2^63, result < 3q.
+  static constexpr int kBaseD = 2;
+  template <int B, bool NEG>
+  __device__ __forceinline__ void basemul(uint32_t (&a)[B], const uint32_t (&b)[B], uint32_t w1,
+                                          uint32_t w2) const {
+    static_assert(B == 4, "sums of B products must fit 64 bits");
+    if (NEG) {  // -w in Montgomery form: (q - w1, (q - w1)(-q^-1) = ~w2 mod 2^32)
+      w1 = q - w1;
+      w2 = ~w2;
+    }
+    uint32_t ar[B], br[B], bz[B];
+#pragma unroll
+    for (int i = 0; i < B; i++) {
+      ar[i] = H ? csub(a[i], 2 * q) : csub(a[i], q);
+      br[i] = H ? csub(csub(b[i], 2 * q), q) : csub(b[i], q);
+    }
+#pragma unroll
+    for (int i = 1; i < B; i++) bz[i] = csub(shoup(b[i], w1, w2), q);
+#pragma unroll
+    for (int k = 0; k < B; k++) {
+      uint64_t s = 0;
+#pragma unroll
+      for (int i = 0; i < B; i++)
+        s += (uint64_t)ar[i] * (i <= k ? br[k - i] : bz[B + k - i]);
+      const uint32_t m = (uint32_t)s * qinv_neg;
+      if (H) {
+        a[k] = csub((uint32_t)((s + (uint64_t)m * q) >> 32), 2 * q);
+      } else {
+        uint64_t t;
+        const bool c = __builtin_add_overflow(s, (uint64_t)m * q, &t);  // value c 2^64 + t
+        const uint32_t hi = (uint32_t)(t >> 32);                      // result < 2.875 q
+        uint32_t d;
+        const bool br2 = __builtin_sub_overflow(hi, 2 * q, &d);
+        a[k] = (c || !br2) ? d : hi;
+      }
+    }
+  }
 };
 using Arith32 = Arith32T<false>;   // q < 2^31
 using Arith32H = Arith32T<true>;   // q < 2^30
@@ -198,6 +243,9 @@ struct Arith32W {
     return redc(p, (uint32_t)p * qinv_neg);
   }
   __device__ __forceinline__ uint32_t canon(uint32_t x) const { return x; }
+  static constexpr int kBaseD = 0;  // sums of two canonical products already exceed 2^64
+  template <int B, bool NEG>
+  __device__ void basemul(uint32_t (&)[B], const uint32_t (&)[B], uint32_t, uint32_t) const {}
 };
 
 // 64-bit arithmetic on a 32-bit VALU.  q < 2^62 leaves two bits of headroom, so butterflies use
@@ -339,6 +387,9 @@ struct Arith64 {
     const uint64_t s = lo + mlo;
     return hi + mhi + (s < lo ? 1 : 0);  // (t + m q) / 2^64 < 2q
   }
+  static constexpr int kBaseD = 0;
+  template <int B, bool NEG>
+  __device__ void basemul(uint64_t (&)[B], const uint64_t (&)[B], uint64_t, uint64_t) const {}
 };
 
 // Twiddle + Shoup companion, stored interleaved so one load fetches both.

@@ -194,6 +194,9 @@ int make_plan(uint32_t n, uint64_t q, uint64_t psi, Plan *P, bool cyclic) {
   const uint64_t f = mulmod(P->inv_n, r_mod_q, q);
   tw_pair(f, q, bits, &P->f, &P->fs);
   tw_pair(mulmod(iw[1], f, q), q, bits, &P->wf, &P->wfs);
+  const uint64_t f4 = mulmod(f, 4, q);
+  tw_pair(f4, q, bits, &P->f4, &P->f4s);
+  tw_pair(mulmod(iw[1], f4, q), q, bits, &P->wf4, &P->wf4s);
   // standalone inverse NTT: plain n^-1 (ntt256.C:12); pointwise product: R^2 mod q
   tw_pair(P->inv_n, q, bits, &P->fi, &P->fis);
   tw_pair(mulmod(iw[1], P->inv_n, q), q, bits, &P->wfi, &P->wfis);

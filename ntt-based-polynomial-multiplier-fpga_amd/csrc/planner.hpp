@@ -34,6 +34,9 @@ struct Plan {
   uint64_t qinv_neg = 0, f = 0, fs = 0, wf = 0, wfs = 0;
   uint64_t fi = 0, fis = 0, wfi = 0, wfis = 0, r2 = 0;  // standalone inverse / pointwise
   uint64_t fu = 0, fus = 0, wfu = 0, wfus = 0;          // unscaled inverse (F = 1)
+  // product with incomplete transforms (kernels.hip base_mult, D = 2): the inverse skips D
+  // stages, so it leaves (n / 2^D) c and the scale is F 2^D
+  uint64_t f4 = 0, f4s = 0, wf4 = 0, wf4s = 0;
   // interleaved {w, w'} pairs (u32 or u64 each), n entries; entry 0 unused
   std::vector<uint8_t> fw, iw;
 };
