@@ -54,6 +54,9 @@
 #define NTTMUL_MIN_WAVES 1
 #endif
 // Ablation switches for tools/kbench timing builds only (results are wrong when set).
+#ifndef NTTMUL_KBENCH_LITE
+#define NTTMUL_KBENCH_LITE 0
+#endif
 #ifndef NTTMUL_ABL_NOLOAD
 #define NTTMUL_ABL_NOLOAD 0
 #endif
@@ -641,6 +644,11 @@ static hipError_t multipass(const LaunchTables &T, const void *a, const void *b,
 hipError_t launch_polymul(const LaunchTables &T, const void *a, const void *b, void *c,
                           size_t batch, int io_bits, void **scr, hipStream_t s) {
   const bool big = T.logn > 12;
+#if NTTMUL_KBENCH_LITE  // tools/kbench quick builds: 32-bit words, q < 2^31, n <= 4096 only
+  if (T.word_bits != 32 || T.q >= (1ull << 31) || big || io_bits != 32) return hipErrorNotSupported;
+  if (NTTMUL_A32H && T.q < (1ull << 30)) return fused<Arith32H, uint32_t>(T, a, b, c, batch, s);
+  return fused<Arith32, uint32_t>(T, a, b, c, batch, s);
+#else
   if (NTTMUL_A32H && T.word_bits == 32 && T.q < (1ull << 30)) {  // Harvey bounds fit
     if (io_bits == 64)
       return big ? multipass<Arith32H, uint64_t>(T, a, b, c, batch, scr, s)
@@ -667,6 +675,7 @@ hipError_t launch_polymul(const LaunchTables &T, const void *a, const void *b, v
                : fused<Arith64, uint32_t>(T, a, b, c, batch, s);
   return big ? multipass<Arith64, uint64_t>(T, a, b, c, batch, scr, s)
              : fused<Arith64, uint64_t>(T, a, b, c, batch, s);
+#endif
 }
 
 template <class A, class TIn, class TOut, int LOGS, int L1, int DIR>
@@ -757,8 +766,12 @@ static hipError_t launch_xform_dir(const LaunchTables &T, const void *in, void *
 
 hipError_t launch_xform(const LaunchTables &T, const void *in, void *out, size_t batch,
                         int io_bits, int inverse, void **scr, hipStream_t s) {
+#if NTTMUL_KBENCH_LITE
+  return hipErrorNotSupported;
+#else
   return inverse ? launch_xform_dir<1>(T, in, out, batch, io_bits, scr, s)
                  : launch_xform_dir<0>(T, in, out, batch, io_bits, scr, s);
+#endif
 }
 
 template <class A, class IO>
@@ -774,6 +787,9 @@ static hipError_t pointwise(const LaunchTables &T, const void *a, const void *b,
 
 hipError_t launch_pointwise(const LaunchTables &T, const void *a, const void *b, void *c,
                             size_t batch, int io_bits, hipStream_t s) {
+#if NTTMUL_KBENCH_LITE
+  return hipErrorNotSupported;
+#else
   const size_t total = batch << T.logn;
   if (!total) return hipSuccess;
   if (T.word_bits == 32 && T.q >= (1ull << 31))
@@ -784,6 +800,7 @@ hipError_t launch_pointwise(const LaunchTables &T, const void *a, const void *b,
                          : pointwise<Arith32, uint32_t>(T, a, b, c, total, s);
   return io_bits == 64 ? pointwise<Arith64, uint64_t>(T, a, b, c, total, s)
                        : pointwise<Arith64, uint32_t>(T, a, b, c, total, s);
+#endif
 }
 
 hipError_t launch_bitrev(const void *in, void *out, uint32_t logn, size_t batch, int io_bits,

@@ -387,9 +387,42 @@ struct Arith64 {
     const uint64_t s = lo + mlo;
     return hi + mhi + (s < lo ? 1 : 0);  // (t + m q) / 2^64 < 2q
   }
-  static constexpr int kBaseD = 0;
+  // Base multiplication of the incomplete transform (see Arith32T::basemul): a = a b 2^-64 in
+  // Z_q[x]/(x^B - z), z = (NEG ? -1 : 1) w, Shoup twiddle (w, w').  a, b, b' = z b canonical,
+  // each output a 128-bit sum of B products < B q^2 < 2^126, one Montgomery reduction:
+  // (S + m q) / 2^64 < q (4q / 2^64 + 1) < 2q.
+#ifndef NTTMUL_A64_BASE
+#define NTTMUL_A64_BASE 1
+#endif
+  static constexpr int kBaseD = NTTMUL_A64_BASE ? 2 : 0;
   template <int B, bool NEG>
-  __device__ void basemul(uint64_t (&)[B], const uint64_t (&)[B], uint64_t, uint64_t) const {}
+  __device__ __forceinline__ void basemul(uint64_t (&a)[B], const uint64_t (&b)[B], uint64_t w,
+                                          uint64_t ws) const {
+    static_assert(B == 4, "B products per 128-bit sum");
+    if (NEG) {  // -w in Shoup form: (q - w, floor((q - w) 2^64 / q) = ~w')
+      w = q - w;
+      ws = ~ws;
+    }
+    uint64_t ar[B], br[B], bz[B];
+#pragma unroll
+    for (int i = 0; i < B; i++) {
+      ar[i] = canon(a[i]);
+      br[i] = canon(b[i]);
+    }
+#pragma unroll
+    for (int i = 1; i < B; i++) bz[i] = csub(shoup(b[i], w, ws), q);
+#pragma unroll
+    for (int k = 0; k < B; k++) {
+      unsigned __int128 s = 0;
+#pragma unroll
+      for (int i = 0; i < B; i++)
+        s += (unsigned __int128)ar[i] * (i <= k ? br[k - i] : bz[B + k - i]);
+      const uint64_t lo = (uint64_t)s, hi = (uint64_t)(s >> 64);
+      const uint64_t m = lo * qinv_neg;
+      // lo + lo64(m q) = 0 mod 2^64: its carry is (lo != 0)
+      a[k] = hi + mulhi64(m, q) + (lo != 0 ? 1 : 0);
+    }
+  }
 };
 
 // Twiddle + Shoup companion, stored interleaved so one load fetches both.
