@@ -63,8 +63,8 @@ def max_over_ranks(x: float, dist, device) -> float:
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--n", type=int, default=4096)
     ap.add_argument("--q", type=int, default=2013265921)
     ap.add_argument("--batch-per-gpu", type=int, default=65536)

@@ -24,7 +24,9 @@
 #include "launch.hpp"
 #include "modarith.hpp"
 
-// LDS regions per polynomial pair (2: a and b exchanged together; 1: in turn, half the LDS)
+// LDS regions per polynomial pair for 32-bit words (2: a and b exchanged together; 1: in turn,
+// half the LDS).  64-bit words always use one region: two would be 68 KiB per block, 2 blocks per
+// CU; one region lets 3-4 blocks share a CU (C5 -6 %, tools/c5_ab.sh)
 #ifndef NTTMUL_LDS_REGIONS
 #define NTTMUL_LDS_REGIONS 2
 #endif
@@ -68,6 +70,9 @@
 #endif
 
 namespace nttmul {
+
+template <class W>
+__host__ __device__ constexpr int lds_regions() { return sizeof(W) == 8 ? 1 : NTTMUL_LDS_REGIONS; }
 
 template <class A>
 struct KParams {
@@ -222,7 +227,7 @@ __device__ __forceinline__ void exchange(W (&x)[16], W (&y)[16], W *lds_x, W *ld
 #endif
   const int bw = Gr::pad(Gr::base(gfrom, j));
   const int br = Gr::pad(Gr::base(gto, j));
-  if (NTTMUL_LDS_REGIONS == 1 && NREG == 2) {  // one region, the two polynomials in turn
+  if (lds_regions<W>() == 1 && NREG == 2) {  // one region, the two polynomials in turn
 #pragma unroll
     for (int k = 0; k < 16; k++) lds_x[bw + Gr::pad(Gr::off(gfrom, k))] = x[k];
     __syncthreads();
@@ -331,7 +336,7 @@ __global__ __launch_bounds__(256, NTTMUL_MIN_WAVES) void k_rows(KParams<A> P, co
   using W = typename A::word;
   using Gr = Groups<LOGS>;
   constexpr int N = Gr::N, TP = N / 16, PB = 256 / TP, G = Gr::G, NP = Gr::NP;
-  __shared__ W lds[PB][NTTMUL_LDS_REGIONS][NP];
+  __shared__ W lds[PB][lds_regions<W>()][NP];
 
   const int pb = threadIdx.x / TP, j = threadIdx.x % TP;
   const size_t u = (size_t)blockIdx.x * PB + pb;
@@ -356,7 +361,7 @@ __global__ __launch_bounds__(256, NTTMUL_MIN_WAVES) void k_rows(KParams<A> P, co
     y[k] = to_word<W>(ld_stream(b + base_l + Gr::off(0, k)));
   }
 #endif
-  W *lx = lds[pb][0], *ly = lds[pb][NTTMUL_LDS_REGIONS - 1];
+  W *lx = lds[pb][0], *ly = lds[pb][lds_regions<W>() - 1];
   constexpr int D = NTTMUL_BASE_D ? A::kBaseD : 0;
   TwPair<W> zw[16];
   fwd_all<A, LOGS, 0, 2, D>(P.ar, x, y, lx, ly, P.fw, j, row, L1, zw);
