@@ -144,6 +144,20 @@ def load_traffic(n: int, q: int, batch: int):
     return None
 
 
+def load_valu_bound(n: int, q: int, batch: int):
+    """VALU-issue bound of the product kernel (profiles/r1_valu_bound.json, tools/valu_bound.py):
+    cycles per wave from the ISA x waves per SIMD / the clock the kernel sustains (PMC)."""
+    path = os.path.join(ROOT, "profiles", "r1_valu_bound.json")
+    try:
+        data = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    for e in data.get("entries", []):
+        if e.get("n") == n and e.get("q") == q and e.get("batch") == batch:
+            return e
+    return None
+
+
 def main(argv=None):
     args = parse(argv)
     import torch
@@ -228,6 +242,12 @@ def main(argv=None):
                          "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": None,
         }
+        vb = load_valu_bound(n, q, batch) if single_launch and wb == 32 else None
+        if vb:  # the bound that binds: integer VALU issue at the sustained clock
+            line["valu_roofline"] = {"bound": "valu", "cycles_per_wave": vb["cycles_per_wave"],
+                                     "valu_per_wave": vb["valu_per_wave"],
+                                     "clock_ghz": vb["clock_ghz"], "bound_ms": vb["valu_bound_ms"],
+                                     "frac": vb["valu_bound_ms"] / kern_ms}
         if args.host_io:
             line["host_io"] = host_io(ctx, a, b, p1 - p0, n, wb)
         if world == 1 and not args.no_cpu_baseline:

@@ -1,0 +1,59 @@
+"""VALU-issue bound of one kernel from its gfx950 ISA listing (the roofline that actually binds the
+product kernel).
+
+    python tools/valu_bound.py <kernels.s> <symbol-substring> <waves-per-launch> <clock-GHz> [kernel-ms]
+
+cycles/wave = sum over the kernel's VALU instructions of the per-opcode SIMD issue cost measured
+by tools/microbench/valu_issue.hip (cycles per wave64 instruction per SIMD, 8 waves/SIMD).  The
+carry/select forms (v_sub_co / v_cndmask, VOP3-encoded with an SGPR-pair carry) are priced at the
+VOP2 rate: in the kernel's mixed instruction stream they measured no slower (the
+hand-scheduled all-VOP2 variant).  The bound is straight-line: every VALU instruction of the
+listing runs once per wave (k_rows has no loops).  bound_ms = cycles/wave x waves per SIMD / clock.
+"""
+import collections
+import json
+import re
+import sys
+
+SIMDS = 1024  # 256 CUs x 4 SIMDs
+
+# cycles per wave64 instruction per SIMD (tools/microbench/valu_issue.hip on MI355X)
+COST = {
+    "v_mad_u64_u32": 4.2, "v_mad_i64_i32": 4.2, "v_mul_lo_u32": 4.2, "v_mul_hi_u32": 4.2,
+    "v_mul_u32_u24": 4.2, "v_mul_hi_u32_u24": 4.2, "v_min_u32": 4.2, "v_max_u32": 4.2,
+    "v_med3_u32": 4.2, "v_lshlrev_b32": 4.2, "v_add3_u32": 4.2, "v_lshl_add_u32": 4.2,
+    "v_lshl_add_u64": 4.2, "v_cmp_ge_u64": 4.2, "v_cmp_gt_u64": 4.2, "v_cmp_lt_u64": 4.2,
+    "v_cmp_eq_u64": 4.2, "v_cmp_ne_u64": 4.2, "v_lshlrev_b64": 4.2, "v_lshrrev_b64": 4.2,
+    "v_fma_f32": 3.8,
+}
+CHEAP = 2.3  # v_add/sub(+co/cndmask), logic, shifts right, moves
+
+
+def cost(op: str) -> float:
+    base = re.sub(r"_e(32|64)$", "", op)
+    return COST.get(base, CHEAP)
+
+
+def main():
+    path, key, waves, ghz = sys.argv[1], sys.argv[2], int(sys.argv[3]), float(sys.argv[4])
+    kms = float(sys.argv[5]) if len(sys.argv) > 5 else None
+    s = open(path).read()
+    m = re.search(r"^(\S*%s\S*):\s*;" % re.escape(key), s, re.M)
+    body = s[m.end():s.index(".Lfunc_end", m.end())]
+    ops = [ln.strip().split()[0] for ln in body.split("\n")
+           if ln.strip().startswith("v_")]
+    hist = collections.Counter(ops)
+    cyc = sum(cost(o) * c for o, c in hist.items())
+    per_simd = waves / SIMDS
+    bound_ms = cyc * per_simd / (ghz * 1e9) * 1e3
+    out = {"kernel": m.group(1), "valu_per_wave": len(ops), "cycles_per_wave": round(cyc, 1),
+           "waves_per_simd": per_simd, "clock_ghz": ghz, "valu_bound_ms": round(bound_ms, 4)}
+    if kms:
+        out["kernel_ms"] = kms
+        out["frac_of_valu_bound"] = round(bound_ms / kms, 4)
+    out["top"] = {o: c for o, c in hist.most_common(12)}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
