@@ -4,11 +4,14 @@ product kernel).
     python tools/valu_bound.py <kernels.s> <symbol-substring> <waves-per-launch> <clock-GHz> [kernel-ms]
 
 cycles/wave = sum over the kernel's VALU instructions of the per-opcode SIMD issue cost measured
-by tools/microbench/valu_issue.hip (cycles per wave64 instruction per SIMD, 8 waves/SIMD).  The
-carry/select forms (v_sub_co / v_cndmask, VOP3-encoded with an SGPR-pair carry) are priced at the
-VOP2 rate: in the kernel's mixed instruction stream they measured no slower (the
-hand-scheduled all-VOP2 variant).  The bound is straight-line: every VALU instruction of the
-listing runs once per wave (k_rows has no loops).  bound_ms = cycles/wave x waves per SIMD / clock.
+by tools/microbench/valu_issue.hip (cycles per wave64 instruction per SIMD, 8 waves/SIMD).
+Instructions that write a carry or read a lane mask (v_*_co_*, v_addc/subb, v_cndmask, v_cmp) are
+priced at CARRY_COST = 3.9 in either encoding (isolated VOP3 forms measure 4.1-4.4; the VCC e32
+pair 2.4 only back to back without the 2-wait-state SGPR hazard), fitted on the compute-only
+ablation (no loads, exchanges or stores; profiles/r1_ablation_clock.txt): 9,680 cycles per wave
+measured, 9,709 predicted; the VCC-forced variant (cvcc) costs the same.  The bound is straight-line: every VALU
+instruction of the listing runs once per wave (k_rows has no loops).
+bound_ms = cycles/wave x waves per SIMD / clock.
 """
 import collections
 import json
@@ -26,11 +29,19 @@ COST = {
     "v_cmp_eq_u64": 4.2, "v_cmp_ne_u64": 4.2, "v_lshlrev_b64": 4.2, "v_lshrrev_b64": 4.2,
     "v_fma_f32": 3.8,
 }
-CHEAP = 2.3  # v_add/sub(+co/cndmask), logic, shifts right, moves
+CHEAP = 2.3  # v_add/sub, logic, shifts right, moves
+# carry-writing / mask-reading instructions: fitted so the compute-only ablation's listing
+# predicts its measured 9,680 cycles per wave (9,709 at 3.9)
+CARRY_COST = 3.9
+
+
+CARRY = re.compile(r"^v_(add|sub|subrev)_co_|^v_(addc|subb|subbrev)_co_|^v_cndmask_|^v_cmp")
 
 
 def cost(op: str) -> float:
     base = re.sub(r"_e(32|64)$", "", op)
+    if CARRY.match(base):
+        return CARRY_COST
     return COST.get(base, CHEAP)
 
 
