@@ -79,7 +79,10 @@ def parse(argv=None):
 
 def cpu_baseline(n: int, q: int, target_s: float):
     """The oracle's psi-merged lazy-Shoup port of the reference's optimized path (oracle/), OpenMP
-    over the batch on this host's cores; bounded sample sized to ~target_s seconds."""
+    over the batch on this host's cores; bounded sample sized to ~target_s seconds.  Beside it
+    (BASELINE.md §3): the ports of the unoptimized CT (ntt256.C:5-13) and GS (:16-24) sequences
+    at the same (n, q), and the reference's own compiled objects as single-core anchors where
+    they can run (n = 256 / 1024, q = 12289; oracle/ref_anchor.c)."""
     import numpy as np
     from oracle import oracle as O
 
@@ -89,14 +92,23 @@ def cpu_baseline(n: int, q: int, target_s: float):
         return None
     per = max(64, threads * 16)
     a, b = O.fill_inputs(n, q, 0, per)
-    a = a.astype(np.uint32)
-    b = b.astype(np.uint32)
-    _, t = P.fast_batch_u32(a, b, threads)              # warm + calibrate
+    a32 = a.astype(np.uint32)
+    b32 = b.astype(np.uint32)
+    _, t = P.fast_batch_u32(a32, b32, threads)          # warm + calibrate
     reps = max(1, int(target_s / max(t, 1e-6)))
     total_t = 0.0
     for _ in range(reps):
-        _, t = P.fast_batch_u32(a, b, threads)
+        _, t = P.fast_batch_u32(a32, b32, threads)
         total_t += t
+    value = per * reps / total_t
+    variants = {}
+    for gs, name in ((False, "ct_unoptimized_port"), (True, "gs_unoptimized_port")):
+        _, t = P.product_batch(a, b, gs, threads)       # warm + calibrate
+        r = max(1, int(0.15 * target_s / max(t, 1e-6)))
+        tt = sum(P.product_batch(a, b, gs, threads)[1] for _ in range(r))
+        variants[name] = {"value": per * r / tt, "unit": "polymults/s",
+                          "us_per_polymult_per_core": tt / (per * r) * threads * 1e6}
+    anchors = {k: {"us_per_polymult": v * 1e6, "cores": 1} for k, v in O.ref_anchors().items()}
     model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -105,10 +117,13 @@ def cpu_baseline(n: int, q: int, target_s: float):
                 break
     except OSError:
         pass
-    return {"value": per * reps / total_t, "unit": "polymults/s", "cores": threads, "kind": "port",
+    return {"value": value, "unit": "polymults/s", "cores": threads, "kind": "port",
+            "us_per_polymult_per_core": threads / value * 1e6,
             "sample": f"{per * reps} polymults (n={n}, q={q}) = {reps} passes over {per} "
                       f"counter-based inputs, OpenMP {threads} threads of {os.cpu_count()} "
-                      f"({model}), {total_t:.1f} s, oracle/nttmul_oracle.c orc_fast_batch_u32"}
+                      f"({model}), {total_t:.1f} s, oracle/nttmul_oracle.c orc_fast_batch_u32",
+            "variants": variants,
+            "reference_anchors": anchors or "oracle/_ref not built (no reference tree)"}
 
 
 def host_io(ctx, a_dev, b_dev, batch: int, n: int, wb: int, reps: int = 3):

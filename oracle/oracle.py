@@ -263,6 +263,51 @@ def ref_available() -> bool:
     return os.path.exists(REF_LIB_PATH)
 
 
+ANCHOR_LIB_PATH = os.path.join(HERE, "_ref", "libref_anchor.so")
+
+
+def ref_anchors(reps256: int = 20000, reps1024: int = 4000, seed: int = SEED) -> dict:
+    """Seconds per product of the reference's own compiled objects (oracle/ref_anchor.c), single
+    thread: the four n = 256 products and the ntt.C generic loops at n = 1024 with planner tables
+    (q = 12289).  Each result is checked against the oracle before its time is reported."""
+    if not os.path.exists(ANCHOR_LIB_PATH):
+        return {}
+    L = ctypes.CDLL(ANCHOR_LIB_PATH)
+    L.anchor_product256.restype = ctypes.c_double
+    L.anchor_product256.argtypes = [ctypes.c_int, _i32p, _i32p, _i32p, ctypes.c_int]
+    L.anchor_product_generic.restype = ctypes.c_double
+    u16p = ctypes.POINTER(ctypes.c_uint16)
+    L.anchor_product_generic.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(u16p),
+                                         _i32p, _i32p, _i32p, ctypes.c_int]
+    out = {}
+    q = 12289
+    P = Plan(256, q, 1002)                     # the reference tables' psi (ntt256_tables.h:20)
+    a, b = fill_inputs(256, q, 0, 1, seed)
+    a32, b32 = a[0].astype(np.int32), b[0].astype(np.int32)
+    want = P.product_merged(a[0], b[0])
+    for i, name in enumerate(("ntt256_product1", "ntt256_product4", "ntt_red256_product1",
+                              "ntt_red256_product4")):
+        c = np.zeros(256, dtype=np.int32)
+        s = L.anchor_product256(i, _pi32(a32), _pi32(b32), _pi32(c), reps256)
+        if np.array_equal(c.astype(np.uint64), want):
+            out[f"{name} n=256 q=12289"] = s
+    n = 1024
+    P = Plan(n, q)
+    names = ("psi_powers", "omega_powers", "omega_powers_rev", "inv_omega_powers",
+             "inv_omega_powers_rev", "scaled_inv_psi_powers")
+    tabs = [np.ascontiguousarray(P.table(k).astype(np.uint16)) for k in names]
+    tp = (u16p * 6)(*[t.ctypes.data_as(u16p) for t in tabs])
+    a, b = fill_inputs(n, q, 0, 1, seed)
+    a32, b32 = a[0].astype(np.int32), b[0].astype(np.int32)
+    want = P.product_merged(a[0], b[0])
+    for gs, name in ((0, "ntt.C CT loops (product1 shape)"), (1, "ntt.C GS loops (product4 shape)")):
+        c = np.zeros(n, dtype=np.int32)
+        s = L.anchor_product_generic(gs, n, tp, _pi32(a32), _pi32(b32), _pi32(c), reps1024)
+        if np.array_equal(c.astype(np.uint64), want):
+            out[f"{name} n=1024 q=12289"] = s
+    return out
+
+
 class Ref:
     """Direct bindings to the reference's own objects (n = 256, q = 12289 products; generic-n
     loops of ntt.C with caller-supplied uint16 tables)."""

@@ -223,3 +223,12 @@ def test_inputs_counter_based():
     a2, b2 = O.fill_inputs(64, 2013265921, 11, 1)
     assert np.array_equal(a[1], a2[0]) and np.array_equal(b[1], b2[0])
     assert int(a.max()) < 2013265921
+
+
+@needs_ref
+def test_reference_anchors_run_and_agree():
+    """bench.py's single-core anchors on the reference's own objects: every anchor is reported
+    only when its product equals the oracle's, so all six keys present = all six agree."""
+    r = O.ref_anchors(reps256=50, reps1024=10)
+    assert len(r) == 6, r
+    assert all(0 < v < 1e-2 for v in r.values())
