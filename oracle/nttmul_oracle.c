@@ -680,6 +680,7 @@ typedef struct {
   uint32_t n, q;
   uint32_t *fw, *fws, *iw, *iws; /* mixed_powers_rev / inv_mixed_powers_rev + Shoup companions */
   uint32_t ninv, ninvs;
+  uint64_t mu;                   /* floor(2^64 / q) (Barrett, pointwise product) */
 } fast_tabs;
 
 static inline uint32_t shoup32(uint32_t x, uint32_t w, uint32_t ws, uint32_t q) {
@@ -701,8 +702,28 @@ static void fast_tabs_make(const orc_plan *P, fast_tabs *F) {
   }
   F->ninv = (uint32_t)P->inv_n;
   F->ninvs = (uint32_t)(((uint64_t)F->ninv << 32) / P->q);
+  F->mu = ~(uint64_t)0 / P->q;
 }
 static void fast_tabs_free(fast_tabs *F) { free(F->fw); free(F->fws); free(F->iw); free(F->iws); }
+
+/* One CT stage block (ntt.C:365-367 butterfly, lazy [0, 2q)) and one GS stage block
+ * (ntt.C:445-447), over d contiguous pairs: restrict-qualified so gcc vectorizes them (AVX2). */
+static inline void fast_ct_block(uint32_t *restrict x0, uint32_t *restrict x1, uint32_t d,
+                                 uint32_t w, uint32_t ws, uint32_t q) {
+  for (uint32_t s = 0; s < d; s++) {
+    uint32_t X = csub(x0[s], q), T = csub(shoup32(x1[s], w, ws, q), q);
+    x0[s] = X + T;
+    x1[s] = X - T + q;
+  }
+}
+static inline void fast_gs_block(uint32_t *restrict x0, uint32_t *restrict x1, uint32_t d,
+                                 uint32_t w, uint32_t ws, uint32_t q) {
+  for (uint32_t s = 0; s < d; s++) {
+    uint32_t X = csub(x0[s], q), Y = csub(x1[s], q);
+    x0[s] = X + Y;
+    x1[s] = shoup32(X - Y + q, w, ws, q);
+  }
+}
 
 static void fast_product(const fast_tabs *F, uint32_t *c, const uint32_t *ain, const uint32_t *bin,
                          uint32_t *a, uint32_t *b) {
@@ -715,29 +736,23 @@ static void fast_product(const fast_tabs *F, uint32_t *c, const uint32_t *ain, c
     uint32_t d = n;
     for (uint32_t t = 1; t < n; t <<= 1) {
       d >>= 1;
-      for (uint32_t j = 0, u = 0; j < t; j++, u += 2 * d) {
-        uint32_t w = F->fw[t + j], ws = F->fws[t + j];
-        for (uint32_t s = u; s < u + d; s++) {
-          uint32_t X = csub(x[s], q), T = csub(shoup32(x[s + d], w, ws, q), q);
-          x[s] = X + T;
-          x[s + d] = X - T + q;
-        }
-      }
+      for (uint32_t j = 0, u = 0; j < t; j++, u += 2 * d)
+        fast_ct_block(x + u, x + u + d, d, F->fw[t + j], F->fws[t + j], q);
     }
   }
-  for (uint32_t i = 0; i < n; i++)
-    c[i] = (uint32_t)(((uint64_t)csub(a[i], q) * csub(b[i], q)) % q);
+  /* mul_array (ntt.C:131-137): Barrett with mu = floor(2^64 / q); p < q^2 < 2^62 gives a
+   * quotient estimate at most 1 low, so r < 2q < 2^32 */
+  const uint64_t mu = F->mu;
+  for (uint32_t i = 0; i < n; i++) {
+    const uint64_t p = (uint64_t)csub(a[i], q) * csub(b[i], q);
+    const uint64_t r = p - (uint64_t)(((u128)p * mu) >> 64) * q;
+    c[i] = csub((uint32_t)r, q);
+  }
   uint32_t t = n;
   for (uint32_t d = 1; d < n; d <<= 1) { /* nttmul_gs_rev2std */
     t >>= 1;
-    for (uint32_t j = 0, u = 0; j < t; j++, u += 2 * d) {
-      uint32_t w = F->iw[t + j], ws = F->iws[t + j];
-      for (uint32_t s = u; s < u + d; s++) {
-        uint32_t X = csub(c[s], q), Y = csub(c[s + d], q);
-        c[s] = X + Y;
-        c[s + d] = shoup32(X - Y + q, w, ws, q);
-      }
-    }
+    for (uint32_t j = 0, u = 0; j < t; j++, u += 2 * d)
+      fast_gs_block(c + u, c + u + d, d, F->iw[t + j], F->iws[t + j], q);
   }
   for (uint32_t i = 0; i < n; i++) c[i] = csub(shoup32(c[i], F->ninv, F->ninvs, q), q);
 }
