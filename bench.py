@@ -67,7 +67,8 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--n", type=int, default=4096)
     ap.add_argument("--q", type=int, default=2013265921)
-    ap.add_argument("--batch-per-gpu", type=int, default=65536)
+    ap.add_argument("--batch-per-gpu", type=int, default=0,
+                    help="0: 65536 (C3) per GPU, or 2^20 / 8 at 8 ranks (C4: batch 2^20 over 8 GPUs)")
     ap.add_argument("--word-bits", type=int, default=0, help="32/64 coefficient storage (0: auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-io", action="store_true",
@@ -153,9 +154,9 @@ def load_traffic(n: int, q: int, batch: int):
         data = json.load(open(path))
     except (OSError, ValueError):
         return None
-    for e in data.get("entries", []):
-        if e.get("n") == n and e.get("q") == q and e.get("batch") == batch:
-            return e.get("hbm_bytes_per_launch")
+    for e in data.get("entries", []):   # per-polymult bytes of a measured batch, scaled
+        if e.get("n") == n and e.get("q") == q and e.get("batch"):
+            return e["hbm_bytes_per_launch"] * batch / e["batch"]
     return None
 
 
@@ -167,9 +168,9 @@ def load_valu_bound(n: int, q: int, batch: int):
         data = json.load(open(path))
     except (OSError, ValueError):
         return None
-    for e in data.get("entries", []):
-        if e.get("n") == n and e.get("q") == q and e.get("batch") == batch:
-            return e
+    for e in data.get("entries", []):   # waves per SIMD scale with the batch
+        if e.get("n") == n and e.get("q") == q and e.get("batch"):
+            return dict(e, valu_bound_ms=e["valu_bound_ms"] * batch / e["batch"])
     return None
 
 
@@ -191,7 +192,8 @@ def main(argv=None):
 
     n, q = args.n, args.q
     wb = args.word_bits or (32 if q < (1 << 32) else 64)
-    batch = args.batch_per_gpu
+    # weak scaling: C3's 65536 polymults per GPU; at 8 ranks the global batch is C4's 2^20
+    batch = args.batch_per_gpu or ((1 << 20) // world if world == 8 else 65536)
     global_batch = batch * world
     p0, p1 = shard(global_batch, rank, world)
 
@@ -245,7 +247,8 @@ def main(argv=None):
             "dtype": "u32" if wb == 32 else "u64",
             "data": "synthetic: splitmix64 counter-based coefficients mod q, generated on device "
                     "(SURVEY §8d, seed 0x4E54544D554C)",
-            "config": {"workload": f"C3: n={n}, q={q}, batch {batch} polymults per GPU "
+            "config": {"workload": f"{'C4' if global_batch == 1 << 20 and world == 8 else 'C3'}: "
+                                   f"n={n}, q={q}, batch {batch} polymults per GPU "
                                    f"(global {global_batch}), device-resident",
                        "n": n, "q": q, "batch_per_gpu": batch, "global_batch": global_batch,
                        "parallelism": f"batch shards x{world}, no collective"},
