@@ -175,6 +175,29 @@ __device__ __forceinline__ void fwd_group(const A &ar, typename A::word (&x)[16]
       if (k & dist) continue;
       const int m = k / ns;
       const int idx = tbase + (Gr::blk(g, j, k) << l) + (m >> (S - l));
+      if constexpr (A::kTyped) {
+        // operand type: bit 2 dist of k says the previous stage of this group wrote it as Y
+        // (N-type); the group's first stage reads P-type; its last writes P-type
+        const bool in_n = l > 0 && (k & (2 * dist));
+        const bool out_p = l == S - SKIP - 1;
+        const TwPair<typename A::word> t = in_n ? tw[idx + (1 << (l1 + LOGS))] : tw[idx];
+        if (out_p) zw[k] = t;
+        const bool xc = NTTMUL_FIRST_XC && g == 0 && l == 0 && l1 == 0;
+#define NTTMUL_CT_T(IN, OUT, XC_)                                 \
+  do {                                                            \
+    ar.template ct_t<IN, OUT, XC_>(x[k], x[k + dist], t.w, t.ws); \
+    if (NPOLY == 2) ar.template ct_t<IN, OUT, XC_>(y[k], y[k + dist], t.w, t.ws); \
+  } while (0)
+        if (xc) {
+          if (out_p) NTTMUL_CT_T(false, true, true); else NTTMUL_CT_T(false, false, true);
+        } else if (in_n) {
+          if (out_p) NTTMUL_CT_T(true, true, false); else NTTMUL_CT_T(true, false, false);
+        } else {
+          if (out_p) NTTMUL_CT_T(false, true, false); else NTTMUL_CT_T(false, false, false);
+        }
+#undef NTTMUL_CT_T
+        continue;
+      }
       const TwPair<typename A::word> t = tw[NTTMUL_ABL_TWMASK ? (idx & NTTMUL_ABL_TWMASK) : idx];
       if (l == S - SKIP - 1) zw[k] = t;
       // global stage 0 of a whole polynomial reads canonical input (the API contract, [0, q)):
@@ -206,6 +229,30 @@ __device__ __forceinline__ void inv_group(const KParams<A> &P, typename A::word 
 #pragma unroll
     for (int k = 0; k < 16; k++) {
       if (k & dist) continue;
+      if constexpr (A::kTyped) {
+        // first stage of the group (inverse order) reads P-type; later ones read the previous
+        // stage's Y registers (bit dist / 2 of k) as N-type; the group's last stage writes P-type
+        const bool in_n = l < S - 1 - SKIP && (k & (dist >> 1));
+        const bool out_p = l == 0;
+        if (SCALE && st == 0) {
+          if (in_n)
+            P.ar.template gs_scaled_t<true>(x[k], x[k + dist], P.f, P.fs, P.wf, P.wfs);
+          else
+            P.ar.template gs_scaled_t<false>(x[k], x[k + dist], P.f, P.fs, P.wf, P.wfs);
+          continue;
+        }
+        const int m = k / ns;
+        const int idx = tbase + (Gr::blk(g, j, k) << l) + (m >> (S - l));
+        const TwPair<typename A::word> t = out_p ? tw[idx] : tw[idx + (1 << (l1 + LOGS))];
+        if (in_n) {
+          if (out_p) P.ar.template gs_t<true, true>(x[k], x[k + dist], t.w, t.ws);
+          else P.ar.template gs_t<true, false>(x[k], x[k + dist], t.w, t.ws);
+        } else {
+          if (out_p) P.ar.template gs_t<false, true>(x[k], x[k + dist], t.w, t.ws);
+          else P.ar.template gs_t<false, false>(x[k], x[k + dist], t.w, t.ws);
+        }
+        continue;
+      }
       if (SCALE && st == 0) {
         P.ar.gs_scaled(x[k], x[k + dist], P.f, P.fs, P.wf, P.wfs);
       } else {
@@ -311,11 +358,21 @@ __device__ __forceinline__ void base_mult(const A &ar, typename A::word (&x)[16]
 #pragma unroll
       for (int i = 0; i < B; i++) r[i] = Gr::reg_of(g, o0 + i);
       const bool neg = (o0 >> D) & 1;
-      const TwPair<typename A::word> z = zw[Gr::reg_of(g, o0 & ~B)];
+      const int kz = Gr::reg_of(g, o0 & ~B);
+      const TwPair<typename A::word> z = zw[kz];
+      // typed arithmetic: the last forward stage (dist 8 >> (S - D - 1)) multiplied N-type
+      // operands, and so kept the centred twiddle, when bit 2 dist of its X register is set
+      constexpr int dl = 8 >> (Gr::S(g) - D - 1);
+      const bool zc = A::kTyped && Gr::S(g) - D - 1 > 0 && (kz & (2 * dl));
       typename A::word a[B], b[B];
 #pragma unroll
       for (int i = 0; i < B; i++) a[i] = x[r[i]], b[i] = y[r[i]];
-      if (neg)
+      if (zc) {
+        if (neg)
+          ar.template basemul<B, true, true>(a, b, z.w, z.ws);
+        else
+          ar.template basemul<B, false, true>(a, b, z.w, z.ws);
+      } else if (neg)
         ar.template basemul<B, true>(a, b, z.w, z.ws);
       else
         ar.template basemul<B, false>(a, b, z.w, z.ws);

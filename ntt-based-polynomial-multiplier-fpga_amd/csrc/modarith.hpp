@@ -23,6 +23,10 @@
 #ifndef NTTMUL_CSUB
 #define NTTMUL_CSUB 2
 #endif
+// typed P/N butterflies for Arith32 (q < 2^31): 1 = on (needs the planner's centred tables)
+#ifndef NTTMUL_TYPED
+#define NTTMUL_TYPED 1
+#endif
 // Arith32 twiddle products: 0 = Shoup (w, floor(w 2^32 / q)), 1 = Montgomery form (planner.cpp
 // emits the matching table pairs; the macro must agree between host and device objects)
 #ifndef NTTMUL_A32_MONT
@@ -38,6 +42,8 @@ template <bool H>
 struct Arith32T {
   using word = uint32_t;
   static constexpr int kBits = 32;
+  // typed butterflies (kernels.hip fwd_group / inv_group): see ct_t below
+  static constexpr bool kTyped = !H && NTTMUL_TYPED && NTTMUL_A32_MONT;
   uint32_t q;
   uint32_t qinv_neg;  // -q^-1 mod 2^32
 
@@ -50,6 +56,13 @@ struct Arith32T {
 #elif NTTMUL_CSUB == 2
     uint32_t d;
     return __builtin_sub_overflow(x, m, &d) ? x : d;
+#elif NTTMUL_CSUB == 3
+    // sign-mask form (m < 2^31, so x - m is a valid int32): v_sub + v_ashr + v_and + v_add
+    // (the shift is opaque asm so the compiler cannot fold the mask back into cmp + cndmask)
+    const uint32_t d = x - m;
+    uint32_t s;
+    asm("v_ashrrev_i32_e32 %0, 31, %1" : "=v"(s) : "v"(d));
+    return d + (s & m);
 #else
     // VOP2 (e32) forms through VCC: the VOP3 forms with an SGPR-pair carry/mask that hipcc
     // otherwise picks issue at ~4.3 cycles each on gfx950, the e32 pair at ~2.4.  The s_nop
@@ -79,6 +92,56 @@ struct Arith32T {
   __device__ __forceinline__ uint32_t shoup(uint32_t x, uint32_t w, uint32_t ws) const {
     uint32_t qh = __umulhi(x, ws);
     return x * w - qh * q;
+  }
+#endif
+#if NTTMUL_A32_MONT
+  // --- typed butterflies (q < 2^31, Montgomery twiddles) -------------------------------------
+  // A register holds a P-type value in [0, 2q) (unsigned) or an N-type value in (-q, q) (int32).
+  // Inside a register group every operand's type is a compile-time fact (bit 2 dist of the
+  // register index says whether the previous stage wrote it as X or Y), so the CT difference
+  // x - t and the GS difference x - y can stay N-type instead of paying "+ q" to stay
+  // non-negative: one VALU instruction less per butterfly.  N-type operands are reduced by
+  // cadd (the carry of y + q is the sign of y) and multiplied by mont_s with the centred
+  // twiddle (w1 in (-q/2, q/2], planner.cpp appends that table after the unsigned one).
+  // Group boundaries (LDS exchanges, the base multiplication, stores) see P-type only.
+  __device__ __forceinline__ static uint32_t cadd(uint32_t x, uint32_t m) {
+    uint32_t e;
+    return __builtin_add_overflow(x, m, &e) ? e : x;
+  }
+  template <bool N>
+  __device__ __forceinline__ uint32_t corr(uint32_t x) const {
+    return N ? cadd(x, q) : csub(x, q);
+  }
+  // y w mod q for y in (-q, q) (int32) and the centred Montgomery pair (w1c, w2c = w1c (-q^-1)):
+  // |y w1c + m q| < q^2 / 2 + 2^31 q, so the result lies in (-0.74 q, 0.74 q).
+  __device__ __forceinline__ uint32_t mont_s(uint32_t y, uint32_t w1c, uint32_t w2c) const {
+    const int32_t m = (int32_t)(y * w2c);
+    const int64_t s = (int64_t)(int32_t)y * (int32_t)w1c + (int64_t)m * (int32_t)q;
+    return (uint32_t)(int32_t)(s >> 32);
+  }
+  // CT on operands of type IN_N (X and Y share it); (w, ws) is the centred pair when IN_N.
+  // Outputs: X' P-type, Y' N-type (OUT_P: P-type, x - t + q, at the end of a register group).
+  template <bool IN_N, bool OUT_P, bool XC = false>
+  __device__ __forceinline__ void ct_t(uint32_t &X, uint32_t &Y, uint32_t w, uint32_t ws) const {
+    const uint32_t x = XC ? X : corr<IN_N>(X);
+    const uint32_t t = IN_N ? cadd(mont_s(Y, w, ws), q) : csub(shoup(Y, w, ws), q);
+    X = x + t;
+    Y = OUT_P ? x - t + q : x - t;
+  }
+  // GS on operands of type IN_N; (w, ws) centred unless OUT_P.  X' P-type, Y' N-type in
+  // (-0.74 q, 0.74 q) (OUT_P: P-type).
+  template <bool IN_N, bool OUT_P>
+  __device__ __forceinline__ void gs_t(uint32_t &X, uint32_t &Y, uint32_t w, uint32_t ws) const {
+    const uint32_t x = corr<IN_N>(X), y = corr<IN_N>(Y);
+    X = x + y;
+    Y = OUT_P ? shoup(x - y + q, w, ws) : mont_s(x - y, w, ws);
+  }
+  template <bool IN_N>
+  __device__ __forceinline__ void gs_scaled_t(uint32_t &X, uint32_t &Y, uint32_t f, uint32_t fs,
+                                              uint32_t wf, uint32_t wfs) const {
+    const uint32_t x = corr<IN_N>(X), y = corr<IN_N>(Y);
+    X = shoup(x + y, f, fs);
+    Y = shoup(x - y + q, wf, wfs);
   }
 #endif
   // Cooley-Tukey butterfly, ntt.C:365-367 pattern: (X, Y) -> (X + Y w, X - Y w).  In/out [0, 2q);
@@ -147,11 +210,15 @@ struct Arith32T {
   //             reach 2^65, its carry is folded into the final conditional subtraction.
   //   H       : a < 2q, b and b' canonical, sum < 2 B q^2 < 2^63, result < 3q.
   static constexpr int kBaseD = 2;
-  template <int B, bool NEG>
+  // ZC: (w1, w2) is the centred pair (the last forward stage multiplied N-type operands by it).
+  template <int B, bool NEG, bool ZC = false>
   __device__ __forceinline__ void basemul(uint32_t (&a)[B], const uint32_t (&b)[B], uint32_t w1,
                                           uint32_t w2) const {
     static_assert(B == 4, "sums of B products must fit 64 bits");
-    if (NEG) {  // -w in Montgomery form: (q - w1, (q - w1)(-q^-1) = ~w2 mod 2^32)
+    if (NEG && ZC) {  // -w centred: (-w1c, -w2c)
+      w1 = 0u - w1;
+      w2 = 0u - w2;
+    } else if (NEG) {  // -w in Montgomery form: (q - w1, (q - w1)(-q^-1) = ~w2 mod 2^32)
       w1 = q - w1;
       w2 = ~w2;
     }
@@ -162,7 +229,15 @@ struct Arith32T {
       br[i] = H ? csub(csub(b[i], 2 * q), q) : csub(b[i], q);
     }
 #pragma unroll
-    for (int i = 1; i < B; i++) bz[i] = csub(shoup(b[i], w1, w2), q);
+    for (int i = 1; i < B; i++) {
+#if NTTMUL_A32_MONT
+      if (ZC && !H) {
+        bz[i] = cadd(mont_s(br[i], w1, w2), q);
+        continue;
+      }
+#endif
+      bz[i] = csub(shoup(b[i], w1, w2), q);
+    }
 #pragma unroll
     for (int k = 0; k < B; k++) {
       uint64_t s = 0;
@@ -193,6 +268,7 @@ using Arith32H = Arith32T<true>;   // q < 2^30
 struct Arith32W {
   using word = uint32_t;
   static constexpr int kBits = 32;
+  static constexpr bool kTyped = false;
   uint32_t q;
   uint32_t qinv_neg;  // -q^-1 mod 2^32
 
@@ -244,7 +320,7 @@ struct Arith32W {
   }
   __device__ __forceinline__ uint32_t canon(uint32_t x) const { return x; }
   static constexpr int kBaseD = 0;  // sums of two canonical products already exceed 2^64
-  template <int B, bool NEG>
+  template <int B, bool NEG, bool ZC = false>
   __device__ void basemul(uint32_t (&)[B], const uint32_t (&)[B], uint32_t, uint32_t) const {}
 };
 
@@ -263,6 +339,7 @@ struct Arith32W {
 struct Arith64 {
   using word = uint64_t;
   static constexpr int kBits = 64;
+  static constexpr bool kTyped = false;
   uint64_t q;
   uint64_t qinv_neg;  // -q^-1 mod 2^64
 
@@ -395,7 +472,7 @@ struct Arith64 {
 #define NTTMUL_A64_BASE 1
 #endif
   static constexpr int kBaseD = NTTMUL_A64_BASE ? 2 : 0;
-  template <int B, bool NEG>
+  template <int B, bool NEG, bool ZC = false>
   __device__ __forceinline__ void basemul(uint64_t (&a)[B], const uint64_t (&b)[B], uint64_t w,
                                           uint64_t ws) const {
     static_assert(B == 4, "B products per 128-bit sum");

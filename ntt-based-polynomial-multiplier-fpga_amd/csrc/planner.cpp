@@ -102,6 +102,24 @@ static void put_pairs(std::vector<uint8_t> &dst, const std::vector<uint64_t> &w,
   }
 }
 
+// Centred Montgomery pairs for the N-type operands of modarith.hpp's typed butterflies: after
+// the n unsigned pairs (w1 in [0, q)), the same twiddles with w1c = w1 - q when w1 > q / 2, as
+// int32 bits, and w2c = w1c (-q^-1) mod 2^32 (= w2 + 1 when shifted).
+static void append_centred(std::vector<uint8_t> &dst, uint32_t n, uint64_t q) {
+  const size_t half = dst.size();
+  dst.resize(2 * half);
+  uint32_t *p = (uint32_t *)dst.data();
+  uint64_t inv = q;
+  for (int i = 0; i < 5; i++) inv *= 2 - q * inv;
+  const uint32_t qinv_neg = (uint32_t)(0 - inv);
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t w1 = p[2 * i];
+    const uint32_t w1c = w1 > q / 2 ? (uint32_t)(w1 - q) : w1;
+    p[2 * n + 2 * i] = w1c;
+    p[2 * n + 2 * i + 1] = w1c * qinv_neg;
+  }
+}
+
 uint64_t smallest_omega(uint32_t n, uint64_t q) {
   if ((q - 1) % n) return 0;
   uint64_t r = 0;
@@ -180,6 +198,10 @@ int make_plan(uint32_t n, uint64_t q, uint64_t psi, Plan *P, bool cyclic) {
   if (bits == 32) {
     put_pairs<uint32_t>(P->fw, fw, q, 32);
     put_pairs<uint32_t>(P->iw, iw, q, 32);
+    if (NTTMUL_A32_MONT && q < (1ull << 31)) {  // Arith32 typed butterflies: centred copies
+      append_centred(P->fw, n, q);
+      append_centred(P->iw, n, q);
+    }
   } else {
     put_pairs<uint64_t>(P->fw, fw, q, 64);
     put_pairs<uint64_t>(P->iw, iw, q, 64);
