@@ -174,6 +174,29 @@ def load_valu_bound(n: int, q: int, batch: int):
     return None
 
 
+def workload_name(n: int, q: int, global_batch: int, world: int) -> str:
+    """BASELINE.json config this run matches, else 'custom'."""
+    if n == 4096 and q < (1 << 32):
+        if world == 8 and global_batch == 1 << 20:
+            return "C4"
+        if global_batch == 65536 * world:
+            return "C3"
+    if n == 1024 and global_batch == 4096 * world:
+        return "C2"
+    if n == 65536 and q >= (1 << 32) and global_batch == 1024 * world:
+        return "C5"
+    return "custom"
+
+
+def arith_name(q: int) -> str:
+    """Kernel arithmetic class the library dispatches to for q (modarith.hpp)."""
+    if q < (1 << 30):
+        return "Arith32H"
+    if q < (1 << 31):
+        return "Arith32"
+    return "Arith32W" if q < (1 << 32) else "Arith64"
+
+
 def main(argv=None):
     args = parse(argv)
     import torch
@@ -247,15 +270,16 @@ def main(argv=None):
             "dtype": "u32" if wb == 32 else "u64",
             "data": "synthetic: splitmix64 counter-based coefficients mod q, generated on device "
                     "(SURVEY §8d, seed 0x4E54544D554C)",
-            "config": {"workload": f"{'C4' if global_batch == 1 << 20 and world == 8 else 'C3'}: "
+            "config": {"workload": f"{workload_name(n, q, global_batch, world)}: "
                                    f"n={n}, q={q}, batch {batch} polymults per GPU "
                                    f"(global {global_batch}), device-resident",
                        "n": n, "q": q, "batch_per_gpu": batch, "global_batch": global_batch,
                        "parallelism": f"batch shards x{world}, no collective"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_rows<Arith32,u32,u32,12,0>" if (single_launch and wb == 32)
-                         else "polymul (all launches of one step)",
+                         "kernel": (f"k_rows<{arith_name(q)},u32,u32,{n.bit_length() - 1},0>"
+                                    if (single_launch and wb == 32)
+                                    else "polymul (all launches of one step)"),
                          "kernel_ms": kern_ms,
                          "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": None,
