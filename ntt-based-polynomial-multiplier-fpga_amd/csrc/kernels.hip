@@ -59,6 +59,10 @@
 #ifndef NTTMUL_KBENCH_LITE
 #define NTTMUL_KBENCH_LITE 0
 #endif
+// column stages of the n = 65536 multi-pass product (4: 16 x 4096 rows, 5: 32 x 2048)
+#ifndef NTTMUL_SPLIT16
+#define NTTMUL_SPLIT16 4
+#endif
 #ifndef NTTMUL_ABL_NOLOAD
 #define NTTMUL_ABL_NOLOAD 0
 #endif
@@ -509,15 +513,15 @@ __global__ __launch_bounds__(256) void k_cols_fwd(KParams<A> P, const TIn *__res
   const size_t p = gid >> logs, col = gid & (ncol - 1);
   const size_t base = (p << (logs + L1)) + col;
   W x[M], y[M];
-#pragma unroll
+#pragma clang loop unroll(full)
   for (int m = 0; m < M; m++) {
     x[m] = (W)a[base + ((size_t)m << logs)];
     y[m] = NPOLY == 2 ? (W)b[base + ((size_t)m << logs)] : W(0);
   }
-#pragma unroll
+#pragma clang loop unroll(full)
   for (int st = 0; st < L1; st++) {
     const int dist = M >> (st + 1);
-#pragma unroll
+#pragma clang loop unroll(full)
     for (int m = 0; m < M; m++) {
       if (m & dist) continue;
       const TwPair<W> t = P.fw[(1 << st) + (m >> (L1 - st))];
@@ -525,7 +529,7 @@ __global__ __launch_bounds__(256) void k_cols_fwd(KParams<A> P, const TIn *__res
       if (NPOLY == 2) P.ar.ct(y[m], y[m + dist], t.w, t.ws);
     }
   }
-#pragma unroll
+#pragma clang loop unroll(full)
   for (int m = 0; m < M; m++) {
     ta[base + ((size_t)m << logs)] = x[m];
     if (NPOLY == 2) tb[base + ((size_t)m << logs)] = y[m];
@@ -545,12 +549,12 @@ __global__ __launch_bounds__(256) void k_cols_inv(KParams<A> P,
   const size_t p = gid >> logs, col = gid & (ncol - 1);
   const size_t base = (p << (logs + L1)) + col;
   W x[M];
-#pragma unroll
+#pragma clang loop unroll(full)
   for (int m = 0; m < M; m++) x[m] = tc[base + ((size_t)m << logs)];
-#pragma unroll
+#pragma clang loop unroll(full)
   for (int st = L1 - 1; st >= 0; st--) {
     const int dist = M >> (st + 1);
-#pragma unroll
+#pragma clang loop unroll(full)
     for (int m = 0; m < M; m++) {
       if (m & dist) continue;
       if (st == 0) {
@@ -561,7 +565,7 @@ __global__ __launch_bounds__(256) void k_cols_inv(KParams<A> P,
       }
     }
   }
-#pragma unroll
+#pragma clang loop unroll(full)
   for (int m = 0; m < M; m++) c[base + ((size_t)m << logs)] = (TOut)P.ar.canon(x[m]);
 }
 
@@ -672,12 +676,11 @@ static hipError_t fused(const LaunchTables &T, const void *a, const void *b, voi
 }
 
 // Multi-pass product, n = 2^logn in (4096, 65536]: rows of 4096, L1 = logn - 12 column stages.
-template <class A, class IO, int L1>
+template <class A, class IO, int L1, int LOGS = 12>
 static hipError_t multipass_l1(const LaunchTables &T, const void *a, const void *b, void *c,
                                size_t batch, void *ta, void *tb, void *tc, hipStream_t s) {
   using W = typename A::word;
   const KParams<A> P = product_params<A>(T);
-  constexpr int LOGS = 12;
   const size_t cols = batch << LOGS;
   const unsigned cblocks = (unsigned)((cols + 255) / 256);
   hipLaunchKernelGGL((k_cols_fwd<A, IO, L1>), dim3(cblocks), dim3(256), 0, s, P, (const IO *)a,
@@ -698,7 +701,10 @@ static hipError_t multipass(const LaunchTables &T, const void *a, const void *b,
     case 13: return multipass_l1<A, IO, 1>(T, a, b, c, batch, scr[0], scr[1], scr[2], s);
     case 14: return multipass_l1<A, IO, 2>(T, a, b, c, batch, scr[0], scr[1], scr[2], s);
     case 15: return multipass_l1<A, IO, 3>(T, a, b, c, batch, scr[0], scr[1], scr[2], s);
-    case 16: return multipass_l1<A, IO, 4>(T, a, b, c, batch, scr[0], scr[1], scr[2], s);
+    case 16:
+      if (NTTMUL_SPLIT16 == 5)  // 32 x 2048: one more stage in the (HBM-bound) column passes
+        return multipass_l1<A, IO, 5, 11>(T, a, b, c, batch, scr[0], scr[1], scr[2], s);
+      return multipass_l1<A, IO, 4>(T, a, b, c, batch, scr[0], scr[1], scr[2], s);
     default: return hipErrorInvalidValue;
   }
 }
