@@ -20,6 +20,10 @@ Q31 = 2013265921            # 15 * 2^27 + 1, the benchmark modulus
 Q30 = 1073479681            # < 2^30
 Q32 = 4293918721            # 0xFFF00001, full 32-bit word
 Q62 = 0x3FFFFFFFFFE80001    # 62-bit, 2^17 | q - 1
+# the ends of the Arith32 range (2^30 < q < 2^31), where the typed butterflies' bounds are
+# tightest (signed Montgomery in (-0.75 q, 0.75 q), unsigned in [0, 2q)); 2^17 | q - 1
+Q31HI = 2147352577
+Q31LO = 1073872897
 
 
 @pytest.fixture(scope="module")
@@ -99,7 +103,7 @@ def test_schoolbook_bigint_golden(golden_dir, torch_cuda):
 
 
 @pytest.mark.parametrize("n", [256, 512, 1024, 2048, 4096])
-@pytest.mark.parametrize("q", [Q31, Q30, Q32, Q62])
+@pytest.mark.parametrize("q", [Q31, Q30, Q32, Q62, Q31HI, Q31LO])
 def test_random_vs_oracle(n, q, torch_cuda):
     """Ragged batch sizes (partial blocks) against the restated psi-merged product."""
     P = O.Plan(n, q)
@@ -122,7 +126,7 @@ def test_random_vs_oracle(n, q, torch_cuda):
 
 
 @pytest.mark.parametrize("n", [8192, 16384, 32768, 65536])
-@pytest.mark.parametrize("q", [Q31, Q30, Q32, Q62])
+@pytest.mark.parametrize("q", [Q31, Q30, Q32, Q62, Q31HI])
 def test_multipass_vs_oracle(n, q, torch_cuda):
     """n > 4096: column pass + fused rows + inverse column pass."""
     P = O.Plan(n, q)
@@ -229,7 +233,7 @@ def test_transforms_ref256_golden(golden_dir, torch_cuda):
 
 
 @pytest.mark.parametrize("n", [256, 1024, 4096, 8192, 65536])
-@pytest.mark.parametrize("q", [Q31, Q30, Q32, Q62])
+@pytest.mark.parametrize("q", [Q31, Q30, Q32, Q62, Q31HI])
 def test_transforms_vs_oracle(n, q, torch_cuda):
     P = O.Plan(n, q)
     ctx = _ctx(n, q)
