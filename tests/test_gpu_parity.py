@@ -190,6 +190,32 @@ def test_full_size_device_path(n, q, word_bits, batch, torch_cuda):
         assert int((c.long() & 0xFFFFFFFF).max()) < q
 
 
+def test_c4_last_rank_slice(torch_cuda):
+    """C4 (n = 4096, 2^20 products over 8 GPUs): the slice rank 7 owns, at its full size
+    (131,072 products from global index 7 * 131,072), generated and multiplied on this device as
+    bench.py does; sampled products against the oracle at their global counter positions."""
+    import bench
+    torch = torch_cuda
+    n, q, world, rank = 4096, Q31, 8, 7
+    p0, p1 = bench.shard(1 << 20, rank, world)
+    count = p1 - p0
+    assert count == 131072
+    ctx = _ctx(n, q)
+    a = torch.empty(count * n, dtype=torch.int32, device="cuda")
+    b = torch.empty_like(a)
+    c = torch.empty_like(a)
+    stream = torch.cuda.current_stream().cuda_stream
+    ctx.fill_random_device(a, b, p0, count, 32, stream=stream)
+    ctx.multiply_device(c, a, b, count, 32, stream=stream)
+    torch.cuda.synchronize()
+    P = O.Plan(n, q)
+    for i in (0, 1, count // 2 + 3, count - 1):
+        ea, eb = O.fill_inputs(n, q, p0 + i, 1)
+        got = _as_np(c[i * n:(i + 1) * n], 32).astype(np.uint64)
+        assert np.array_equal(got, P.product_merged(ea[0], eb[0])), i
+    assert int((c.long() & 0xFFFFFFFF).max()) < q
+
+
 def test_validate_flag(torch_cuda):
     ctx = _ctx(1024, Q31, validate=True)
     a, b = O.fill_inputs(1024, Q31, 0, 2)
