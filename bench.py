@@ -6,7 +6,8 @@ synthetic polynomials already resident in HBM (generated on the device from the 
 splitmix64 stream of SURVEY §8d, so every rank owns a contiguous slice [p0, p0 + batch) of one
 global batch and no input crosses PCIe or xGMI).  Scaling is weak: each GPU multiplies
 --batch-per-gpu polynomials per step; shards are independent, there is no collective on the data
-path (torch.distributed only provides the barrier and the max-over-ranks time).
+path and no RCCL at all: torch.distributed runs on gloo over CPU tensors and provides only the
+barrier and the max-over-ranks time.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n 4096] [--q 2013265921]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
@@ -51,10 +52,11 @@ def timed_steps(step, steps: int, warmup: int, sync, barrier):
     return time.perf_counter() - t0
 
 
-def max_over_ranks(x: float, dist, device) -> float:
-    """Max of a per-rank float over the process group (identity when not distributed)."""
+def max_over_ranks(x: float, dist, device=None) -> float:
+    """Max of a per-rank float over the (gloo) process group; identity when not distributed.
+    A CPU tensor: the control plane never touches the GPUs or RCCL."""
     import torch
-    t = torch.tensor([x], dtype=torch.float64, device=device)
+    t = torch.tensor([x], dtype=torch.float64)
     if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
@@ -75,6 +77,13 @@ def parse(argv=None):
                     help="also time the host-buffer ABI path (PCIe-inclusive; never the value)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target wall time of the CPU-baseline sample")
+    ap.add_argument("--rotate", type=int, default=0,
+                    help="cycle the steps over this many distinct (a, b, c) buffer sets, so a "
+                         "batch smaller than the Infinity Cache is still read from HBM "
+                         "(0: auto = enough sets for 3 x 256 MiB when the batch fits in it, else 1)")
+    ap.add_argument("--dump-samples", default="",
+                    help="write <prefix>.rank<r>.npz with sampled products of this rank's slice "
+                         "(checked against the oracle by tests/test_gpu_parity.py)")
     return ap.parse_args(argv)
 
 
@@ -147,31 +156,44 @@ def host_io(ctx, a_dev, b_dev, batch: int, n: int, wb: int, reps: int = 3):
                     f"{reps}; reported beside, never the bench value"}
 
 
-def load_traffic(n: int, q: int, batch: int):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), if one matches."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def _profile_entry(name: str, n: int, q: int, code_object: str):
+    """The entry of profiles/<name> measured on this (n, q) and this build's device code
+    (nttmul.code_object_id), or None: a profile of another build is never reported."""
     try:
-        data = json.load(open(path))
+        data = json.load(open(os.path.join(ROOT, "profiles", name)))
     except (OSError, ValueError):
         return None
-    for e in data.get("entries", []):   # per-polymult bytes of a measured batch, scaled
-        if e.get("n") == n and e.get("q") == q and e.get("batch"):
-            return e["hbm_bytes_per_launch"] * batch / e["batch"]
+    for e in data.get("entries", []):
+        if (e.get("n") == n and e.get("q") == q and e.get("batch")
+                and e.get("code_object") == code_object):
+            return e
     return None
 
 
-def load_valu_bound(n: int, q: int, batch: int):
-    """VALU-issue bound of the product kernel (profiles/r1_valu_bound.json, tools/valu_bound.py):
-    cycles per wave from the ISA x waves per SIMD / the clock the kernel sustains (PMC)."""
-    path = os.path.join(ROOT, "profiles", "r1_valu_bound.json")
+def load_traffic(n: int, q: int, batch: int, code_object: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary of this build
+    (profiles/pmc_traffic.json, tools/summarize_profile.py), scaled to this batch; with its
+    source, or (None, reason)."""
+    e = _profile_entry("pmc_traffic.json", n, q, code_object)
+    if e is None:
+        return None, f"no PMC profile of code object {code_object} at n={n}, q={q}"
+    return (e["hbm_bytes_per_launch"] * batch / e["batch"],
+            f"profiles/pmc_traffic.json <- {e['source']} (code object {code_object}, "
+            f"batch {e['batch']}, {e['method']})")
+
+
+def load_valu_bound(n: int, q: int, code_object: str):
+    """VALU issue cycles per wave of the product kernel of this build, from its ISA listing
+    (profiles/valu_bound.json, tools/valu_bound.py), or None."""
+    return _profile_entry("valu_bound.json", n, q, code_object)
+
+
+def code_object_or_none():
+    import nttmul
     try:
-        data = json.load(open(path))
+        return nttmul.code_object_id()
     except (OSError, ValueError):
         return None
-    for e in data.get("entries", []):   # waves per SIMD scale with the batch
-        if e.get("n") == n and e.get("q") == q and e.get("batch"):
-            return dict(e, valu_bound_ms=e["valu_bound_ms"] * batch / e["batch"])
-    return None
 
 
 def workload_name(n: int, q: int, global_batch: int, world: int) -> str:
@@ -197,6 +219,11 @@ def arith_name(q: int) -> str:
     return "Arith32W" if q < (1 << 32) else "Arith64"
 
 
+IC_BYTES = 256 << 20        # MI355X Infinity Cache (MI355X_MICROARCH.md)
+MAX_CLOCK_GHZ = 2.4         # MI355X max engine clock (MI355X_MICROARCH.md)
+SIMDS = 1024                # 256 CUs x 4 SIMDs
+
+
 def main(argv=None):
     args = parse(argv)
     import torch
@@ -208,10 +235,13 @@ def main(argv=None):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    if world > 1:  # control plane only (barrier, max of a float): gloo on CPU tensors, no RCCL
+        dist.init_process_group("gloo")
+    # one rank per GPU; more ranks than GPUs (the 2-rank rehearsal on a 1-GPU box) share them
+    ndev = torch.cuda.device_count()
+    devno = local % max(ndev, 1)
+    torch.cuda.set_device(devno)
+    dev = torch.device("cuda", devno)
 
     n, q = args.n, args.q
     wb = args.word_bits or (32 if q < (1 << 32) else 64)
@@ -219,18 +249,27 @@ def main(argv=None):
     batch = args.batch_per_gpu or ((1 << 20) // world if world == 8 else 65536)
     global_batch = batch * world
     p0, p1 = shard(global_batch, rank, world)
+    count = p1 - p0
+    wbytes = wb // 8
+    alg_bytes = 3 * n * wbytes * count                    # read a, b + write c, per launch
+    rotate = args.rotate or (-(-3 * IC_BYTES // alg_bytes) if alg_bytes <= IC_BYTES else 1)
 
-    ctx = nttmul.Context(n, q, ndev=1, first_dev=local)
+    ctx = nttmul.Context(n, q, ndev=1, first_dev=devno)
     dt = torch.int32 if wb == 32 else torch.int64
-    a = torch.empty((p1 - p0) * n, dtype=dt, device=dev)
-    b = torch.empty_like(a)
-    c = torch.empty_like(a)
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
-    ctx.fill_random_device(a, b, p0, p1 - p0, wb, seed=SEED, stream=sptr)
+    sets = []
+    for _ in range(rotate):   # identical inputs in every set (same counter range)
+        a = torch.empty(count * n, dtype=dt, device=dev)
+        b = torch.empty_like(a)
+        ctx.fill_random_device(a, b, p0, count, wb, seed=SEED, stream=sptr)
+        sets.append((a, b, torch.empty_like(a)))
+    state = {"i": 0}
 
     def step():
-        ctx.multiply_device(c, a, b, p1 - p0, wb, stream=sptr)
+        a, b, c = sets[state["i"] % rotate]
+        state["i"] += 1
+        ctx.multiply_device(c, a, b, count, wb, stream=sptr)
 
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
@@ -247,15 +286,24 @@ def main(argv=None):
     wall = timed_steps(timed_step, args.steps, args.warmup, lambda: torch.cuda.synchronize(dev),
                        (lambda: dist.barrier()) if world > 1 else (lambda: None))
     kern_ms = ev0.elapsed_time(ev1) / args.steps
-    wall_max = max_over_ranks(wall, dist if world > 1 else None, dev)
+    wall_max = max_over_ranks(wall, dist if world > 1 else None)
+
+    if args.dump_samples:  # sampled products of this rank's slice, at their global positions
+        import numpy as np
+        a, b, c = sets[(state["i"] - 1) % rotate]
+        idx = sorted({0, 1, count // 2, count - 1})
+        host = c.view(count, n).cpu().numpy()
+        rows = host.view(np.uint32 if wb == 32 else np.uint64)[idx].astype(np.uint64)
+        np.savez(f"{args.dump_samples}.rank{rank}.npz", p0=p0, p1=p1, idx=np.array(idx),
+                 c=rows, n=n, q=q, world=world, global_batch=global_batch)
 
     if rank == 0:
         value = global_batch * args.steps / wall_max
-        wbytes = wb // 8
-        alg_bytes = 3 * n * wbytes * (p1 - p0)           # read a, b + write c, per launch
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9     # GB/s
         single_launch = n <= 4096
-        traffic = load_traffic(n, q, batch)
+        co = code_object_or_none()
+        traffic, traffic_source = load_traffic(n, q, count, co) if co else (None, "no code object")
+        resident = alg_bytes * rotate <= IC_BYTES
         line = {
             "metric": METRIC,
             "value": value,
@@ -277,21 +325,37 @@ def main(argv=None):
                        "parallelism": f"batch shards x{world}, no collective"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": traffic_source,
                          "kernel": (f"k_rows<{arith_name(q)},u32,u32,{n.bit_length() - 1},0>"
                                     if (single_launch and wb == 32)
                                     else "polymul (all launches of one step)"),
                          "kernel_ms": kern_ms,
-                         "alg_bytes_per_launch": alg_bytes},
+                         "alg_bytes_per_launch": alg_bytes,
+                         "buffer_sets": rotate,
+                         "cache_resident": resident},
+            "build": {"code_object": co},
             "cpu_baseline": None,
         }
-        vb = load_valu_bound(n, q, batch) if single_launch and wb == 32 else None
-        if vb:  # the bound that binds: integer VALU issue at the sustained clock
-            line["valu_roofline"] = {"bound": "valu", "cycles_per_wave": vb["cycles_per_wave"],
-                                     "valu_per_wave": vb["valu_per_wave"],
-                                     "clock_ghz": vb["clock_ghz"], "bound_ms": vb["valu_bound_ms"],
-                                     "frac": vb["valu_bound_ms"] / kern_ms}
+        if rotate > 1:
+            line["roofline"]["note"] = (
+                f"one step's a, b, c ({alg_bytes / 2**20:.0f} MiB) fit the 256 MiB Infinity "
+                f"Cache; the steps cycle over {rotate} buffer sets ({rotate * alg_bytes / 2**20:.0f}"
+                " MiB) so inputs come from HBM as in a batch that does not fit")
+        vb = load_valu_bound(n, q, co) if (co and single_launch and wb == 32) else None
+        if vb:  # the bound that binds: integer VALU issue, from this build's ISA
+            waves_per_simd = count * (n // 16) / 64 / SIMDS
+            bound_ms = vb["cycles_per_wave"] * waves_per_simd / (MAX_CLOCK_GHZ * 1e9) * 1e3
+            line["valu_roofline"] = {
+                "bound": "valu", "cycles_per_wave": vb["cycles_per_wave"],
+                "valu_per_wave": vb["valu_per_wave"], "waves_per_simd": waves_per_simd,
+                "clock_ghz": MAX_CLOCK_GHZ, "bound_ms": bound_ms, "frac": bound_ms / kern_ms,
+                "implied_clock_ghz": vb["cycles_per_wave"] * waves_per_simd / (kern_ms * 1e6),
+                "source": f"profiles/valu_bound.json (code object {co}): the ISA listing priced "
+                          "at measured issue costs, at the 2.4 GHz max clock; implied_clock_ghz "
+                          "= the clock at which the kernel would run exactly at that issue bound"}
         if args.host_io:
-            line["host_io"] = host_io(ctx, a, b, p1 - p0, n, wb)
+            a, b, _ = sets[0]
+            line["host_io"] = host_io(ctx, a, b, count, n, wb)
         if world == 1 and not args.no_cpu_baseline:
             try:
                 line["cpu_baseline"] = cpu_baseline(n, q, args.cpu_seconds)
@@ -299,6 +363,7 @@ def main(argv=None):
                 line["cpu_baseline"] = {"error": str(e)}
         print(json.dumps(line), flush=True)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
 
 

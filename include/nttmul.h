@@ -10,7 +10,7 @@
  * everywhere else.
  *
  * Replaces, one-for-one:
- *   - Software path: ntt256_product1 / ntt256_product4 (NTT/ntt256.h:270-271) and
+ *   - Software path: ntt256_product1 / ntt256_product4 (NTT/ntt256.h:85-86) and
  *     ntt_red256_product1 / ntt_red256_product4 (NTT-RED/ntt_red256.h:87,90) — compat shims below.
  *   - FPGA path: Software_Hardware_Comunnicator/linux_app/NTT_PCIECommunicationv2.c:109-252
  *     NTT_HARDWARE_EXE and the Terasic driver it drives (PCIE.c:59-103):
@@ -95,7 +95,9 @@ int nttmul_multiply_batch_u64(nttmul_ctx *ctx, uint64_t *c, const uint64_t *a, c
 /* Device-resident batch on HIP device `dev` (must be one of the context's devices), enqueued on
  * `stream` (a hipStream_t of that device; NULL is the device's null stream, as everywhere in HIP).
  * word_bits = 32 or 64 selects uint32_t or uint64_t coefficient storage.  Asynchronous: returns
- * after the launch; order it with the caller's other work through `stream`. */
+ * after the launch; order it with the caller's other work through `stream`.  Calls on different
+ * streams may be mixed: for n > 4096 (and the reordered transforms) the context's scratch is
+ * handed from one call to the next by a HIP event, so such calls run in enqueue order. */
 int nttmul_multiply_batch_device(nttmul_ctx *ctx, void *c, const void *a, const void *b,
                                  size_t batch, int word_bits, int dev, void *stream);
 

@@ -8,7 +8,7 @@
 //   mode-3 SendCommand + WaitForDoneAll polling (:211-215, :83-107)   -> launch + stream sync
 //   DmaFifoRead(C) (:220-224)                                          -> hipMemcpyAsync D2H
 //   szError + goto cleanup / return FALSE (:175-178, :242-251)         -> negative status codes
-// and provides the software path's entry points (ntt256_product1/4, NTT/ntt256.h:270-271) as
+// and provides the software path's entry points (ntt256_product1/4, NTT/ntt256.h:85-86) as
 // compat shims.  There is no CPU fallback anywhere in this library.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -33,19 +33,33 @@ constexpr int kMaxDev = 16;
 constexpr int kSlots = 3;                     // host-path pipeline depth per device
 constexpr size_t kChunkBytes = 8u << 20;      // host-path chunk, per operand
 
+// Multi-pass scratch (n > 4096: the column/row intermediates) and the bit-reversed copy of a
+// reordered transform's input.  Sized for a sub-batch of mp_chunk polynomials, not the whole
+// batch, so the intermediates of one sub-batch stay in the 256 MiB Infinity Cache between the
+// column and row passes.  Every use is ordered after the previous one by `ev`, whatever stream
+// it was enqueued on: two device-API calls on different streams (or two host-path slots) never
+// overwrite each other's intermediates.
+struct Scratch {
+  void *buf[3] = {nullptr, nullptr, nullptr};
+  size_t bytes = 0;
+  void *perm = nullptr;
+  size_t perm_bytes = 0;
+  hipEvent_t ev = nullptr;                    // recorded after the last enqueued use
+  bool used = false;
+  hipStream_t last = nullptr;                 // stream of that use
+};
+
 struct DevState {
   int id = -1;
   hipStream_t stream = nullptr;
   void *fw = nullptr, *iw = nullptr;
-  void *scr[3] = {nullptr, nullptr, nullptr};
-  size_t scr_bytes = 0;
-  void *perm = nullptr;                       // bit-reversed copy of a transform's input
-  size_t perm_bytes = 0;
-  // host-buffer path: kSlots pipeline slots, each with a stream, pinned host staging and device
-  // buffers for a, b, c (run_host)
+  Scratch dscr;                               // device-resident API calls
+  // host-buffer path: kSlots pipeline slots, each with a stream, pinned host staging, device
+  // buffers for a, b, c and its own scratch (run_host)
   hipStream_t xs[kSlots] = {};
   void *pin[kSlots][3] = {};
   void *dbuf[kSlots][3] = {};
+  Scratch sscr[kSlots];
   size_t slot_bytes = 0;
   int *flag = nullptr;                        // range-check result
   int cus = 0;                                // compute units (persistent grid sizing)
@@ -105,8 +119,11 @@ DevState *find_dev(nttmul_ctx *ctx, int dev) {
   return nullptr;
 }
 
-int ensure(nttmul_ctx *ctx, void **bufs, int nb, size_t *have, size_t need) {
+// (Re)allocate nb buffers of at least `need` bytes; `sc`'s last use must have completed before
+// the old ones are freed.
+int ensure(nttmul_ctx *ctx, Scratch &sc, void **bufs, int nb, size_t *have, size_t need) {
   if (*have >= need) return NTTMUL_OK;
+  if (sc.used) HIP_TRY(ctx, hipEventSynchronize(sc.ev));
   for (int i = 0; i < nb; i++) {
     if (bufs[i]) (void)hipFree(bufs[i]);
     bufs[i] = nullptr;
@@ -115,6 +132,39 @@ int ensure(nttmul_ctx *ctx, void **bufs, int nb, size_t *have, size_t need) {
   for (int i = 0; i < nb; i++) HIP_TRY(ctx, hipMalloc(&bufs[i], need));
   *have = need;
   return NTTMUL_OK;
+}
+
+// Polynomials per multi-pass / reordered-transform sub-batch: NTTMUL_MP_CHUNK_MB (default 32) MiB
+// per scratch buffer.  Three buffers of one C5 sub-batch (64 x 512 KiB each) plus its a, b and c
+// slices stay well inside the Infinity Cache.
+size_t sub_batch(size_t poly_bytes, size_t batch) {
+  static const size_t mb = [] {
+    const char *e = getenv("NTTMUL_MP_CHUNK_MB");
+    long v = e ? atol(e) : 32;
+    return (size_t)(v > 0 ? v : 32);
+  }();
+  return std::max<size_t>(1, std::min(batch, (mb << 20) / poly_bytes));
+}
+
+int scratch_acquire(nttmul_ctx *ctx, Scratch &sc, hipStream_t s) {
+  if (!sc.ev) HIP_TRY(ctx, hipEventCreateWithFlags(&sc.ev, hipEventDisableTiming));
+  if (sc.used && sc.last != s) HIP_TRY(ctx, hipStreamWaitEvent(s, sc.ev, 0));
+  return NTTMUL_OK;
+}
+
+int scratch_release(nttmul_ctx *ctx, Scratch &sc, hipStream_t s) {
+  HIP_TRY(ctx, hipEventRecord(sc.ev, s));
+  sc.used = true;
+  sc.last = s;
+  return NTTMUL_OK;
+}
+
+void scratch_free(Scratch &sc) {
+  if (sc.used) (void)hipEventSynchronize(sc.ev);
+  for (void *p : {sc.buf[0], sc.buf[1], sc.buf[2], sc.perm})
+    if (p) (void)hipFree(p);
+  if (sc.ev) (void)hipEventDestroy(sc.ev);
+  sc = Scratch();
 }
 
 // Transforms are OP_XFORM + an NTTMUL_XF_* mode (direction | order | scaling).
@@ -127,10 +177,10 @@ enum Op {
 };
 constexpr unsigned kXfModes = NTTMUL_XF_INVERSE | NTTMUL_XF_REV2STD | NTTMUL_XF_UNSCALED;
 
-// Enqueue one device-resident batch of `op` on d (current device must be d.id).  b is unused by
-// the transforms.
-int run_device(nttmul_ctx *ctx, DevState &d, int op, void *c, const void *a, const void *b,
-               size_t batch, int io_bits, hipStream_t s) {
+// Enqueue one device-resident batch of `op` on d (current device must be d.id), using scratch sc
+// where the op needs it.  b is unused by the transforms.
+int run_device(nttmul_ctx *ctx, DevState &d, Scratch &sc, int op, void *c, const void *a,
+               const void *b, size_t batch, int io_bits, hipStream_t s) {
   const Plan &P = ctx->plan;
   if (!batch) return NTTMUL_OK;
   if (io_bits != 32 && io_bits != 64) return NTTMUL_EINVAL;
@@ -147,40 +197,55 @@ int run_device(nttmul_ctx *ctx, DevState &d, int op, void *c, const void *a, con
       return NTTMUL_ERANGE;
     }
   }
-  if (P.logn > 12) {
-    const size_t need = batch * (size_t)P.n * (P.word_bits / 8);
-    int st = ensure(ctx, d.scr, 3, &d.scr_bytes, need);
-    if (st) return st;
-  }
   LaunchTables T = tables_for(ctx, d);
+  const size_t io_poly = (size_t)P.n * (io_bits / 8), w_poly = (size_t)P.n * (P.word_bits / 8);
+  bool inv = false, reorder = false;
   if (op >= OP_XFORM) {
     const unsigned mode = (unsigned)(op - OP_XFORM);
     if (mode & ~kXfModes) return NTTMUL_EINVAL;
-    const bool inv = mode & NTTMUL_XF_INVERSE, rev_in = mode & NTTMUL_XF_REV2STD;
+    inv = mode & NTTMUL_XF_INVERSE;
+    // the kernels run forward std2rev and inverse rev2std; the other orders are the same
+    // transform between two bit-reversal permutations (rev2std = P o std2rev o P, verified on
+    // the reference's own loops: tests/golden/ref256_wrappers.npz)
+    reorder = inv != ((mode & NTTMUL_XF_REV2STD) != 0);
     if (mode & NTTMUL_XF_UNSCALED) {
       if (!inv) return NTTMUL_EINVAL;
       T.fi = P.fu; T.fis = P.fus; T.wfi = P.wfu; T.wfis = P.wfus;
     }
-    // the kernels run forward std2rev and inverse rev2std; the other orders are the same
-    // transform between two bit-reversal permutations (rev2std = P o std2rev o P, verified on
-    // the reference's own loops: tests/golden/ref256_wrappers.npz)
-    if (inv == rev_in) {
-      HIP_TRY(ctx, launch_xform(T, a, c, batch, io_bits, inv, d.scr, s));
-    } else {
-      int st = ensure(ctx, &d.perm, 1, &d.perm_bytes, batch * (size_t)P.n * (io_bits / 8));
-      if (st) return st;
-      HIP_TRY(ctx, launch_bitrev(a, d.perm, P.logn, batch, io_bits, s));
-      HIP_TRY(ctx, launch_xform(T, d.perm, c, batch, io_bits, inv, d.scr, s));
-      HIP_TRY(ctx, launch_bitrev(c, c, P.logn, batch, io_bits, s));
-    }
+  } else if (op != OP_MULTIPLY && op != OP_POINTWISE) {
+    return NTTMUL_EINVAL;
+  }
+  const bool multipass = P.logn > 12 && op != OP_POINTWISE;
+  if (!multipass && !reorder) {  // one launch over the whole batch, no scratch
+    if (op == OP_MULTIPLY) HIP_TRY(ctx, launch_polymul(T, a, b, c, batch, io_bits, sc.buf, s));
+    else if (op == OP_POINTWISE) HIP_TRY(ctx, launch_pointwise(T, a, b, c, batch, io_bits, s));
+    else HIP_TRY(ctx, launch_xform(T, a, c, batch, io_bits, inv, sc.buf, s));
     return NTTMUL_OK;
   }
-  switch (op) {
-    case OP_MULTIPLY: HIP_TRY(ctx, launch_polymul(T, a, b, c, batch, io_bits, d.scr, s)); break;
-    case OP_POINTWISE: HIP_TRY(ctx, launch_pointwise(T, a, b, c, batch, io_bits, s)); break;
-    default: return NTTMUL_EINVAL;
+  // sub-batches through the scratch (1024 products of 512 KiB in 16 sub-batches)
+  const size_t chunk = sub_batch(multipass ? w_poly : io_poly, batch);
+  int st = scratch_acquire(ctx, sc, s);
+  if (st) return st;
+  if (multipass && (st = ensure(ctx, sc, sc.buf, 3, &sc.bytes, chunk * w_poly))) return st;
+  if (reorder && (st = ensure(ctx, sc, &sc.perm, 1, &sc.perm_bytes, chunk * io_poly))) return st;
+  for (size_t p = 0; p < batch && !st; p += chunk) {
+    const size_t cnt = std::min(chunk, batch - p);
+    const char *ap = (const char *)a + p * io_poly;
+    const char *bp = b ? (const char *)b + p * io_poly : nullptr;
+    char *cp = (char *)c + p * io_poly;
+    hipError_t e;
+    if (op == OP_MULTIPLY) {
+      e = launch_polymul(T, ap, bp, cp, cnt, io_bits, sc.buf, s);
+    } else if (!reorder) {
+      e = launch_xform(T, ap, cp, cnt, io_bits, inv, sc.buf, s);
+    } else if ((e = launch_bitrev(ap, sc.perm, P.logn, cnt, io_bits, s)) == hipSuccess &&
+               (e = launch_xform(T, sc.perm, cp, cnt, io_bits, inv, sc.buf, s)) == hipSuccess) {
+      e = launch_bitrev(cp, cp, P.logn, cnt, io_bits, s);
+    }
+    if (e != hipSuccess) st = fail(ctx, e, "sub-batch launch");
   }
-  return NTTMUL_OK;
+  const int rel = scratch_release(ctx, sc, s);
+  return st ? st : rel;
 }
 
 // memcpy split over a few host threads for large blocks (the staging copies bound the
@@ -342,8 +407,8 @@ int run_host(nttmul_ctx *ctx, int op, void *c, const void *a, const void *b, siz
         st = fail(ctx, e, "hipMemcpyAsync H2D");
         break;
       }
-      if ((st = run_device(ctx, d, op, d.dbuf[s][2], d.dbuf[s][0], d.dbuf[s][1], cnt, io_bits,
-                           d.xs[s])))
+      if ((st = run_device(ctx, d, d.sscr[s], op, d.dbuf[s][2], d.dbuf[s][0], d.dbuf[s][1], cnt,
+                           io_bits, d.xs[s])))
         break;
       e = hipMemcpyAsync(d.pin[s][2], d.dbuf[s][2], bytes, hipMemcpyDeviceToHost, d.xs[s]);
       if (e != hipSuccess) {
@@ -452,9 +517,11 @@ void nttmul_destroy(nttmul_ctx *ctx) {
         if (d.pin[k][m]) (void)hipHostFree(d.pin[k][m]);
         if (d.dbuf[k][m]) (void)hipFree(d.dbuf[k][m]);
       }
+      scratch_free(d.sscr[k]);
       if (d.xs[k]) (void)hipStreamDestroy(d.xs[k]);
     }
-    for (void *p : {d.fw, d.iw, (void *)d.flag, d.scr[0], d.scr[1], d.scr[2], d.perm})
+    scratch_free(d.dscr);
+    for (void *p : {d.fw, d.iw, (void *)d.flag})
       if (p) (void)hipFree(p);
     if (d.stream) (void)hipStreamDestroy(d.stream);
   }
@@ -532,7 +599,7 @@ static int device_op(nttmul_ctx *ctx, int op, void *c, const void *a, const void
   if (!d) return NTTMUL_ENODEV;
   DeviceGuard guard;
   HIP_TRY(ctx, hipSetDevice(d->id));
-  return run_device(ctx, *d, op, c, a, b, batch, word_bits, (hipStream_t)stream);
+  return run_device(ctx, *d, d->dscr, op, c, a, b, batch, word_bits, (hipStream_t)stream);
 }
 
 int nttmul_multiply_batch_device(nttmul_ctx *ctx, void *c, const void *a, const void *b,

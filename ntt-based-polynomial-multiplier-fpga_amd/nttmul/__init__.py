@@ -2,7 +2,7 @@
 
 This is the reference-side binding a Python caller uses: it exposes the reference's product entry
 points with their names and argument meaning (ntt256_product1/4, ntt_red256_product1/4:
-NTT/ntt256.h:270-271, NTT-RED/ntt_red256.h:87,90 — output array c, inputs a, b, n = 256,
+NTT/ntt256.h:85-86, NTT-RED/ntt_red256.h:87,90 — output array c, inputs a, b, n = 256,
 q = 12289) plus the generic batched API multiply(a, b) for any (n, q).  All compute runs in
 lib/libnttmul.so on the GPU; there is no CPU fallback: if the library or a GPU is missing the calls
 raise.
@@ -128,6 +128,31 @@ def load_library() -> ctypes.CDLL:
         getattr(lib, name).restype = None
     _LIB = lib
     return lib
+
+
+def code_object_id(path: str = LIB_PATH) -> str:
+    """Identity of the device code in libnttmul.so: sha256 (16 hex digits) of its .hip_fatbin
+    section, the gfx950 code objects of every kernel.  Host-only changes keep it; any kernel
+    change alters it.  bench.py keys the committed PMC/ISA profiles (profiles/) by it, so a
+    profile of another build is never reported as this build's."""
+    import hashlib
+    import struct
+    with open(path, "rb") as f:
+        elf = f.read()
+    if elf[:4] != b"\x7fELF" or elf[4] != 2:
+        raise ValueError(f"{path}: not an ELF64 file")
+    shoff, = struct.unpack_from("<Q", elf, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", elf, 0x3A)
+
+    def sec(i):
+        name, _, _, _, off, size = struct.unpack_from("<IIQQQQ", elf, shoff + i * shentsize)
+        return name, off, size
+    _, stroff, _ = sec(shstrndx)
+    for i in range(shnum):
+        name, off, size = sec(i)
+        if elf[stroff + name:elf.index(b"\0", stroff + name)] == b".hip_fatbin":
+            return hashlib.sha256(elf[off:off + size]).hexdigest()[:16]
+    raise ValueError(f"{path}: no .hip_fatbin section")
 
 
 def exported_symbols() -> list:

@@ -660,6 +660,7 @@ static inline uint64_t splitmix64(uint64_t x) {
 /* a[p][i] = splitmix64(seed + 2 n (p0+p) + i) mod q ; b[p][i] = ... + n + i */
 void orc_fill_inputs(uint64_t *a, uint64_t *b, uint32_t n, uint64_t q, uint64_t seed,
                      uint64_t p0, uint64_t count) {
+#pragma omp parallel for schedule(static)
   for (uint64_t p = 0; p < count; p++) {
     uint64_t base = seed + 2ull * n * (p0 + p);
     for (uint32_t i = 0; i < n; i++) {

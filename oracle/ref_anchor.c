@@ -11,7 +11,7 @@
 #include <string.h>
 #include <time.h>
 
-/* the reference's entry points (NTT/ntt256.h:270-271, NTT-RED/ntt_red256.h:87,90, NTT/ntt.h) */
+/* the reference's entry points (NTT/ntt256.h:85-86, NTT-RED/ntt_red256.h:87,90, NTT/ntt.h) */
 void ntt256_product1(int32_t *c, int32_t *a, int32_t *b);
 void ntt256_product4(int32_t *c, int32_t *a, int32_t *b);
 void ntt_red256_product1(int32_t *c, int32_t *a, int32_t *b);

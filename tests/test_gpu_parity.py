@@ -1,8 +1,9 @@
 """GPU parity tests: the HIP path (through the C ABI) against the oracle and the golden fixtures.
 
-Bit-exact integer results are required everywhere.  Sizes are those the oracle finishes in
-seconds; at BASELINE.json's full sizes the tests check sampled polymults (inputs are counter-based,
-so the oracle regenerates any one) and size-independent properties (linearity, ragged batches).
+Bit-exact integer results are required everywhere.  At BASELINE.json's full sizes (C2, C3, the C4
+rank-7 slice, C5) every product of the batch is compared with the oracle's OpenMP batch product on
+the host cores (inputs are counter-based, so the oracle regenerates the whole batch); smaller cases
+use the restated reference loops directly.
 """
 import json
 import os
@@ -126,18 +127,24 @@ def test_random_vs_oracle(n, q, torch_cuda):
 
 
 @pytest.mark.parametrize("n", [8192, 16384, 32768, 65536])
-@pytest.mark.parametrize("q", [Q31, Q30, Q32, Q62, Q31HI])
+@pytest.mark.parametrize("q", [Q31, Q30, Q32, Q62, Q31HI, Q31LO])
 def test_multipass_vs_oracle(n, q, torch_cuda):
-    """n > 4096: column pass + fused rows + inverse column pass."""
+    """n > 4096: column pass + fused rows + inverse column pass, ragged batch of 3 (and 17 at
+    n = 8192) against the restated reference product (OpenMP batch) and evaluation at roots."""
     P = O.Plan(n, q)
     ctx = _ctx(n, q)
     assert ctx.info.kernel == 2
-    a, b = O.fill_inputs(n, q, 7, 2)
-    a[1] = q - 1
-    dt = np.uint32 if q < (1 << 32) else np.uint64
-    c = ctx.multiply(a.astype(dt), b.astype(dt)).astype(np.uint64)
-    for i in range(2):
-        assert np.array_equal(c[i], P.product_merged(a[i], b[i])), (n, q, i)
+    for batch in ((3, 17) if n == 8192 else (3,)):
+        a, b = O.fill_inputs(n, q, 7 + batch, batch)
+        a[1] = q - 1
+        b[2] = 0; b[2, n - 1] = 1                    # multiply by x^(n-1): a negacyclic rotation
+        dt = np.uint32 if q < (1 << 32) else np.uint64
+        c = ctx.multiply(a.astype(dt), b.astype(dt)).astype(np.uint64)
+        ref = P.product_batch(a, b)[0].reshape(batch, n)
+        bad = np.flatnonzero((c != ref).any(axis=1))
+        assert bad.size == 0, (n, q, batch, bad[:8])
+        rot = np.concatenate([(q - a[2, 1:]) % q, a[2, :1]]).astype(np.uint64)  # a x^(n-1)
+        assert np.array_equal(c[2], rot)
     assert P.eval_check(c[0], a[0], b[0], points=2) == 0
 
 
@@ -150,11 +157,39 @@ def _as_np(t, word_bits):
     return arr.view(np.uint32 if word_bits == 32 else np.uint64)
 
 
+def _oracle_batch(P, q, a, b):
+    """The oracle's whole-batch product (OpenMP over the host cores): the lazy-Shoup port for
+    q < 2^31 (checked against the restated reference in test_oracle.py), else the restated
+    P4 sequence (ntt256.C:16-24 on the generic ntt.C loops) in 128-bit arithmetic."""
+    if q < (1 << 31):
+        return P.fast_batch_u32(a.astype(np.uint32), b.astype(np.uint32))[0].astype(np.uint64)
+    return P.product_batch(a, b)[0]
+
+
+def _check_whole_batch(n, q, word_bits, p0, count, a, b, c, chunk=8192):
+    """Every product of a device batch (global counter positions p0 .. p0 + count) against the
+    oracle, in host chunks: inputs regenerated and compared, products recomputed and compared.
+    Returns the number of products checked."""
+    P = O.Plan(n, q)
+    checked = 0
+    for s0 in range(0, count, chunk):
+        cnt = min(chunk, count - s0)
+        ea, eb = O.fill_inputs(n, q, p0 + s0, cnt)
+        sl = slice(s0 * n, (s0 + cnt) * n)
+        assert np.array_equal(_as_np(a[sl], word_bits).reshape(cnt, n).astype(np.uint64), ea)
+        assert np.array_equal(_as_np(b[sl], word_bits).reshape(cnt, n).astype(np.uint64), eb)
+        got = _as_np(c[sl], word_bits).reshape(cnt, n).astype(np.uint64)
+        bad = np.flatnonzero((got != _oracle_batch(P, q, ea, eb)).any(axis=1))
+        assert bad.size == 0, f"{bad.size} mismatching products, first at {p0 + s0 + bad[0]}"
+        checked += cnt
+    return checked
+
+
 @pytest.mark.parametrize("n,q,word_bits,batch", [(4096, Q31, 32, 65536), (1024, Q31, 32, 4096),
-                                                  (65536, Q62, 64, 1024)])
+                                                  (65536, Q62, 64, 1024), (8192, Q31, 32, 2500)])
 def test_full_size_device_path(n, q, word_bits, batch, torch_cuda):
-    """BASELINE configs C2/C3/C5 at full size on device-resident data: sampled polymults against
-    the oracle (inputs regenerated from the counter) and linearity over the whole batch."""
+    """BASELINE configs C3, C2 and C5 at full size on device-resident data (plus n = 8192 over
+    three multi-pass sub-batches): every product against the oracle, bit-exact."""
     torch = torch_cuda
     ctx = _ctx(n, q)
     dt = _torch_dtype(torch, word_bits)
@@ -165,35 +200,13 @@ def test_full_size_device_path(n, q, word_bits, batch, torch_cuda):
     ctx.fill_random_device(a, b, 0, batch, word_bits, stream=stream)
     ctx.multiply_device(c, a, b, batch, word_bits, stream=stream)
     torch.cuda.synchronize()
-    P = O.Plan(n, q)
-    rng = np.random.default_rng(n + batch)
-    for p in sorted(set([0, batch - 1] + list(rng.integers(0, batch, 2)))):
-        ea, eb = O.fill_inputs(n, q, int(p), 1)
-        assert np.array_equal(_as_np(a[p * n:(p + 1) * n], word_bits).astype(np.uint64), ea[0])
-        got = _as_np(c[p * n:(p + 1) * n], word_bits).astype(np.uint64)
-        assert np.array_equal(got, P.product_merged(ea[0], eb[0])), p
-    # linearity over the whole batch: (a + a') * b == a*b + a'*b  (mod q), checked on the GPU
-    if word_bits == 32:
-        a2 = torch.empty_like(a)
-        d = torch.empty_like(a)
-        ctx.fill_random_device(a2, d, batch, batch, word_bits, stream=stream)  # fresh a'
-        s = ((a.long() & 0xFFFFFFFF) + (a2.long() & 0xFFFFFFFF)) % q
-        s32 = s.to(torch.int32)
-        c_s = torch.empty_like(a)
-        c_2 = torch.empty_like(a)
-        ctx.multiply_device(c_s, s32, b, batch, word_bits, stream=stream)
-        ctx.multiply_device(c_2, a2, b, batch, word_bits, stream=stream)
-        torch.cuda.synchronize()
-        lhs = c_s.long() & 0xFFFFFFFF
-        rhs = ((c.long() & 0xFFFFFFFF) + (c_2.long() & 0xFFFFFFFF)) % q
-        assert torch.equal(lhs, rhs)
-        assert int((c.long() & 0xFFFFFFFF).max()) < q
+    assert _check_whole_batch(n, q, word_bits, 0, batch, a, b, c) == batch
 
 
 def test_c4_last_rank_slice(torch_cuda):
     """C4 (n = 4096, 2^20 products over 8 GPUs): the slice rank 7 owns, at its full size
     (131,072 products from global index 7 * 131,072), generated and multiplied on this device as
-    bench.py does; sampled products against the oracle at their global counter positions."""
+    bench.py does; every product against the oracle at its global counter position."""
     import bench
     torch = torch_cuda
     n, q, world, rank = 4096, Q31, 8, 7
@@ -208,12 +221,29 @@ def test_c4_last_rank_slice(torch_cuda):
     ctx.fill_random_device(a, b, p0, count, 32, stream=stream)
     ctx.multiply_device(c, a, b, count, 32, stream=stream)
     torch.cuda.synchronize()
-    P = O.Plan(n, q)
-    for i in (0, 1, count // 2 + 3, count - 1):
-        ea, eb = O.fill_inputs(n, q, p0 + i, 1)
-        got = _as_np(c[i * n:(i + 1) * n], 32).astype(np.uint64)
-        assert np.array_equal(got, P.product_merged(ea[0], eb[0])), i
-    assert int((c.long() & 0xFFFFFFFF).max()) < q
+    assert _check_whole_batch(n, q, 32, p0, count, a, b, c) == count
+
+
+def test_device_calls_on_two_streams(torch_cuda):
+    """Two multi-pass products enqueued back to back on two different streams share the
+    context's scratch (nttmul.cpp Scratch): the second waits for the first's sub-batches."""
+    torch = torch_cuda
+    n, q, batch = 16384, Q31, 200
+    ctx = _ctx(n, q)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    a = torch.empty(batch * n, dtype=torch.int32, device="cuda")
+    b = torch.empty_like(a)
+    a2, b2 = torch.empty_like(a), torch.empty_like(a)
+    c, c2 = torch.empty_like(a), torch.empty_like(a)
+    ctx.fill_random_device(a, b, 0, batch, 32, stream=s1.cuda_stream)
+    ctx.fill_random_device(a2, b2, batch, batch, 32, stream=s2.cuda_stream)
+    torch.cuda.synchronize()
+    for _ in range(3):
+        ctx.multiply_device(c, a, b, batch, 32, stream=s1.cuda_stream)
+        ctx.multiply_device(c2, a2, b2, batch, 32, stream=s2.cuda_stream)
+    torch.cuda.synchronize()
+    assert _check_whole_batch(n, q, 32, 0, batch, a, b, c) == batch
+    assert _check_whole_batch(n, q, 32, batch, batch, a2, b2, c2) == batch
 
 
 def test_validate_flag(torch_cuda):
@@ -351,10 +381,12 @@ def test_time_testing_gpu_app(golden_dir, torch_cuda):
     assert "Batch 1024" in out
 
 
-@pytest.mark.parametrize("n,q,batch", [(4096, Q31, 1537), (256, Q30, 20000), (1024, Q62, 1100)])
+@pytest.mark.parametrize("n,q,batch", [(4096, Q31, 1537), (256, Q30, 20000), (1024, Q62, 1100),
+                                       (8192, Q31, 600), (65536, Q31, 70), (65536, Q62, 40)])
 def test_host_path_pipeline(n, q, batch, torch_cuda):
     """The host-buffer ABI path streams 8 MiB chunks through 3 pipeline slots (nttmul.cpp
-    run_host): several chunks, a partial last chunk and slot reuse, every product checked."""
+    run_host): several chunks, a partial last chunk and slot reuse, every product checked.  At
+    n > 4096 the slots' multi-pass products run concurrently, each on its own scratch."""
     ctx = _ctx(n, q)
     a, b = O.fill_inputs(n, q, 11, batch)
     dt = np.uint32 if q < (1 << 32) else np.uint64
@@ -430,3 +462,36 @@ def test_transform_modes_device(torch_cuda):
         ctx.transform_device(back, f, inv, batch, 32, stream=s)
         torch.cuda.synchronize()
         assert torch.equal(back, a)
+
+
+def test_bench_two_ranks_on_one_gpu(tmp_path, torch_cuda):
+    """bench.py's N > 1 path as the driver launches it (torch.distributed.run, one process per
+    rank, gloo control plane), with both ranks on this box's GPU(s): the JSON line reports the
+    global batch, and the products each rank dumps from its own slice equal the oracle's at their
+    global counter positions (rank 1 owns [batch, 2 batch))."""
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    batch = 4096
+    prefix = str(tmp_path / "samples")
+    out = subprocess.run(
+        [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+         "--master-addr", "127.0.0.1", "--master-port", str(port),
+         os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+         "--no-cpu-baseline", "--batch-per-gpu", str(batch), "--dump-samples", prefix],
+        capture_output=True, text=True, timeout=300, cwd=root)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["config"]["global_batch"] == 2 * batch
+    assert line["config"]["batch_per_gpu"] == batch and line["value"] > 0
+    P = O.Plan(4096, Q31)
+    for r in range(2):
+        d = np.load(f"{prefix}.rank{r}.npz")
+        assert int(d["p0"]) == r * batch and int(d["p1"]) == (r + 1) * batch
+        for i, row in zip(d["idx"], d["c"]):
+            ea, eb = O.fill_inputs(4096, Q31, int(d["p0"]) + int(i), 1)
+            assert np.array_equal(row, P.product_merged(ea[0], eb[0])), (r, int(i))

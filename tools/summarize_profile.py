@@ -39,6 +39,7 @@ for k in out:
 json.dump(out, open(dst + "_pmc.json", "w"), indent=1)
 
 cfg = bench["config"]
+entry_co = bench.get("build", {}).get("code_object")
 main = "k_rows" if "k_rows" in out else sorted(out)[0]
 m = out[main]
 fetch = 2.0 * m["FETCH_SIZE"] * 1024
@@ -46,8 +47,10 @@ write = m["WRITE_SIZE"] * 1024
 tpath = os.path.join(os.path.dirname(dst) or ".", "pmc_traffic.json")
 table = json.load(open(tpath)) if os.path.exists(tpath) else {"entries": []}
 table["entries"] = [e for e in table["entries"]
-                    if not (e["n"] == cfg["n"] and e["q"] == cfg["q"] and e["batch"] == cfg["batch_per_gpu"])]
+                    if not (e["n"] == cfg["n"] and e["q"] == cfg["q"] and e["batch"] == cfg["batch_per_gpu"]
+                            and e.get("code_object") == entry_co)]
 entry = {"n": cfg["n"], "q": cfg["q"], "batch": cfg["batch_per_gpu"], "kernel": main,
+         "code_object": bench.get("build", {}).get("code_object"),
          "hbm_bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
          "alg_bytes_per_launch": bench["roofline"]["alg_bytes_per_launch"],
          "traffic_over_alg": (fetch + write) / bench["roofline"]["alg_bytes_per_launch"],

@@ -2,6 +2,11 @@
 product kernel).
 
     python tools/valu_bound.py <kernels.s> <symbol-substring> <waves-per-launch> <clock-GHz> [kernel-ms]
+        [--record N Q BATCH]
+
+--record adds the result to profiles/valu_bound.json keyed by (N, Q) and the code object id of the
+current lib/libnttmul.so (nttmul.code_object_id; build the listing from the same tree with
+`make asm`), which bench.py looks up for its valu_roofline field.
 
 cycles/wave = sum over the kernel's VALU instructions of the per-opcode SIMD issue cost measured
 by tools/microbench/valu_issue.hip (cycles per wave64 instruction per SIMD, 8 waves/SIMD).
@@ -46,8 +51,14 @@ def cost(op: str) -> float:
 
 
 def main():
-    path, key, waves, ghz = sys.argv[1], sys.argv[2], int(sys.argv[3]), float(sys.argv[4])
-    kms = float(sys.argv[5]) if len(sys.argv) > 5 else None
+    argv = sys.argv[1:]
+    record = None
+    if "--record" in argv:
+        i = argv.index("--record")
+        record = [int(x) for x in argv[i + 1:i + 4]]
+        argv = argv[:i] + argv[i + 4:]
+    path, key, waves, ghz = argv[0], argv[1], int(argv[2]), float(argv[3])
+    kms = float(argv[4]) if len(argv) > 4 else None
     s = open(path).read()
     m = re.search(r"^(\S*%s\S*):\s*;" % re.escape(key), s, re.M)
     body = s[m.end():s.index(".Lfunc_end", m.end())]
@@ -63,6 +74,21 @@ def main():
         out["kernel_ms"] = kms
         out["frac_of_valu_bound"] = round(bound_ms / kms, 4)
     out["top"] = {o: c for o, c in hist.most_common(12)}
+    if record:
+        import os
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        sys.path.insert(0, os.path.join(root, "ntt-based-polynomial-multiplier-fpga_amd"))
+        import nttmul
+        out.update(n=record[0], q=record[1], batch=record[2],
+                   code_object=nttmul.code_object_id(),
+                   source="tools/valu_bound.py on `make asm` (build/kernels.s) of this tree")
+        tpath = os.path.join(root, "profiles", "valu_bound.json")
+        table = json.load(open(tpath)) if os.path.exists(tpath) else {"entries": []}
+        table["entries"] = [e for e in table["entries"]
+                            if not (e["n"] == out["n"] and e["q"] == out["q"]
+                                    and e.get("code_object") == out["code_object"])]
+        table["entries"].append(out)
+        json.dump(table, open(tpath, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
 
