@@ -134,15 +134,16 @@ int ensure(nttmul_ctx *ctx, Scratch &sc, void **bufs, int nb, size_t *have, size
   return NTTMUL_OK;
 }
 
-// Polynomials per multi-pass / reordered-transform sub-batch: NTTMUL_MP_CHUNK_MB (default 32) MiB
-// per scratch buffer.  Three buffers of one C5 sub-batch (64 x 512 KiB each) plus its a, b and c
-// slices stay well inside the Infinity Cache.
+// Polynomials per multi-pass / reordered-transform sub-batch: NTTMUL_MP_CHUNK_MB (default 512) MiB
+// per scratch buffer (C5: the whole 1024-product batch in one pass).  Smaller sub-batches keep a
+// sub-batch's intermediates in the 256 MiB Infinity Cache but cost more than they save: C5 at
+// 8/16/32/64/128 MiB ran 2.86/1.91/1.60/1.48/1.40 ms against 1.36 ms in one pass
+// (gpurun_out/r2a) — each sub-batch launch is a single generation of blocks.  The
+// bound also caps scratch memory for very large batches.
 size_t sub_batch(size_t poly_bytes, size_t batch) {
-  static const size_t mb = [] {
-    const char *e = getenv("NTTMUL_MP_CHUNK_MB");
-    long v = e ? atol(e) : 32;
-    return (size_t)(v > 0 ? v : 32);
-  }();
+  const char *e = getenv("NTTMUL_MP_CHUNK_MB");
+  const long v = e ? atol(e) : 512;
+  const size_t mb = v > 0 ? (size_t)v : 512;
   return std::max<size_t>(1, std::min(batch, (mb << 20) / poly_bytes));
 }
 

@@ -64,8 +64,19 @@ bool go(Board *B) {
     return false;
   }
   const uint64_t q = B->params[2 * wc];
+  if (q < 3 || !nttmul_is_prime(q)) {  // before any "% q": q = 0 from the stream must not trap
+    snprintf(B->err, sizeof(B->err), "mode-0 stream: q = %llu is not an odd prime",
+             (unsigned long long)q);
+    return false;
+  }
   const uint64_t r = B->params[0] % q, wr = B->params[1] % q;
-  if (q < 3 || !r) return false;
+  if (!r) return false;
+  // the board multiplies whatever the FIFOs delivered: reduce A and B into [0, q) as its
+  // modular datapath does, so the validated-input contract of nttmul_multiply holds
+  for (uint32_t i = 0; i < kN; i++) {
+    B->a[i] = (uint32_t)(B->a[i] % q);
+    B->b[i] = (uint32_t)(B->b[i] % q);
+  }
   const uint64_t omega = nttmul::mulmod(wr, nttmul::powmod(r, q - 2, q), q);
   nttmul_ctx *&ctx = B->ctx[{q, omega}];
   if (!ctx) {
@@ -123,7 +134,7 @@ int PCIE_Write32(int h, int bar, unsigned int addr, unsigned int data) {
     }
     return 1;
   }
-  if (addr + 4 > B->ram.size()) return 0;
+  if ((size_t)addr + 4 > B->ram.size()) return 0;
   memcpy(&B->ram[addr], &data, 4);
   return 1;
 }
@@ -136,7 +147,7 @@ int PCIE_Read32(int h, int bar, unsigned int addr, unsigned int *data) {
     *data = (B->busy & 1) | ((B->done & 1) << 1);
     return 1;
   }
-  if (addr + 4 > B->ram.size()) return 0;
+  if ((size_t)addr + 4 > B->ram.size()) return 0;
   memcpy(data, &B->ram[addr], 4);
   return 1;
 }
@@ -144,14 +155,14 @@ int PCIE_Read32(int h, int bar, unsigned int addr, unsigned int *data) {
 int PCIE_Write16(int h, int, unsigned int addr, unsigned short v) {
   std::lock_guard<std::mutex> l(g_mu);
   Board *B = board(h);
-  if (!B || addr + 2 > B->ram.size()) return 0;
+  if (!B || (size_t)addr + 2 > B->ram.size()) return 0;
   memcpy(&B->ram[addr], &v, 2);
   return 1;
 }
 int PCIE_Read16(int h, int, unsigned int addr, unsigned short *v) {
   std::lock_guard<std::mutex> l(g_mu);
   Board *B = board(h);
-  if (!B || !v || addr + 2 > B->ram.size()) return 0;
+  if (!B || !v || (size_t)addr + 2 > B->ram.size()) return 0;
   memcpy(v, &B->ram[addr], 2);
   return 1;
 }

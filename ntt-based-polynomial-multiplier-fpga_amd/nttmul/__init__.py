@@ -179,6 +179,25 @@ def _ptr(x) -> int:
     return int(x)
 
 
+def _dev_arg(x, batch: int, n: int, word_bits: int, dev: int) -> int:
+    """Device pointer of an operand of a *_device call, after checking what the C ABI cannot:
+    a torch tensor must hold at least batch * n words of word_bits on HIP device `dev`
+    (a raw integer address is passed through unchecked, as in C)."""
+    if word_bits not in (32, 64):
+        raise ValueError("word_bits must be 32 or 64")
+    if hasattr(x, "data_ptr"):
+        if not x.is_contiguous():
+            raise ValueError("device operands must be contiguous")
+        if x.element_size() * 8 != word_bits:
+            raise ValueError(f"tensor of {x.element_size() * 8}-bit elements for word_bits={word_bits}")
+        if x.numel() < batch * n:
+            raise ValueError(f"tensor of {x.numel()} words < batch * n = {batch * n}")
+        if x.device.type != "cuda" or x.device.index != dev:
+            raise ValueError(f"tensor on {x.device}, context call on device {dev}")
+        return x.data_ptr()
+    return _ptr(x)
+
+
 class Context:
     """An (n, q) multiplier bound to one or more HIP devices (≙ an opened FPGA handle)."""
 
@@ -273,7 +292,8 @@ class Context:
     def transform_device(self, out, x, mode: int, batch: int, word_bits: int,
                          dev: Optional[int] = None, stream: int = 0):
         dev = self.first_dev if dev is None else dev
-        self._check(self._lib.nttmul_transform_device(self._h, mode, _ptr(out), _ptr(x), batch,
+        args = [_dev_arg(t, batch, self.n, word_bits, dev) for t in (out, x)]
+        self._check(self._lib.nttmul_transform_device(self._h, mode, *args, batch,
                                                       word_bits, dev, stream or None))
 
     def pointwise(self, a, b, dtype=None) -> np.ndarray:
@@ -281,6 +301,8 @@ class Context:
         dtype = dtype or self.io_dtype
         a = np.ascontiguousarray(a, dtype=dtype)
         b = np.ascontiguousarray(b, dtype=dtype)
+        if a.shape != b.shape or a.shape[-1] != self.n:
+            raise ValueError("a and b must both have shape [..., n]")
         c = np.empty_like(a)
         w = "u32" if dtype == np.uint32 else "u64"
         fn = getattr(self._lib, f"nttmul_pointwise_batch_{w}")
@@ -290,32 +312,37 @@ class Context:
     def forward_device(self, out, a, batch: int, word_bits: int, dev: Optional[int] = None,
                        stream: int = 0):
         dev = self.first_dev if dev is None else dev
-        self._check(self._lib.nttmul_forward_batch_device(self._h, _ptr(out), _ptr(a), batch,
+        args = [_dev_arg(t, batch, self.n, word_bits, dev) for t in (out, a)]
+        self._check(self._lib.nttmul_forward_batch_device(self._h, *args, batch,
                                                           word_bits, dev, stream or None))
 
     def inverse_device(self, out, a, batch: int, word_bits: int, dev: Optional[int] = None,
                        stream: int = 0):
         dev = self.first_dev if dev is None else dev
-        self._check(self._lib.nttmul_inverse_batch_device(self._h, _ptr(out), _ptr(a), batch,
+        args = [_dev_arg(t, batch, self.n, word_bits, dev) for t in (out, a)]
+        self._check(self._lib.nttmul_inverse_batch_device(self._h, *args, batch,
                                                           word_bits, dev, stream or None))
 
     def pointwise_device(self, c, a, b, batch: int, word_bits: int, dev: Optional[int] = None,
                          stream: int = 0):
         dev = self.first_dev if dev is None else dev
-        self._check(self._lib.nttmul_pointwise_batch_device(self._h, _ptr(c), _ptr(a), _ptr(b),
+        args = [_dev_arg(t, batch, self.n, word_bits, dev) for t in (c, a, b)]
+        self._check(self._lib.nttmul_pointwise_batch_device(self._h, *args,
                                                             batch, word_bits, dev, stream or None))
 
     def multiply_device(self, c, a, b, batch: int, word_bits: int, dev: Optional[int] = None,
                         stream: int = 0):
         """Device-resident batch (pointers or torch tensors on `dev`), enqueued on `stream`."""
         dev = self.first_dev if dev is None else dev
-        self._check(self._lib.nttmul_multiply_batch_device(self._h, _ptr(c), _ptr(a), _ptr(b), batch,
+        args = [_dev_arg(t, batch, self.n, word_bits, dev) for t in (c, a, b)]
+        self._check(self._lib.nttmul_multiply_batch_device(self._h, *args, batch,
                                                            word_bits, dev, stream or None))
 
     def fill_random_device(self, a, b, p0: int, count: int, word_bits: int, seed: int = SEED,
                            dev: Optional[int] = None, stream: int = 0):
         dev = self.first_dev if dev is None else dev
-        self._check(self._lib.nttmul_fill_random_device(self._h, _ptr(a), _ptr(b), p0, count, seed,
+        args = [_dev_arg(t, count, self.n, word_bits, dev) for t in (a, b)]
+        self._check(self._lib.nttmul_fill_random_device(self._h, *args, p0, count, seed,
                                                         word_bits, dev, stream or None))
 
 

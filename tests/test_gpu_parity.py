@@ -185,12 +185,16 @@ def _check_whole_batch(n, q, word_bits, p0, count, a, b, c, chunk=8192):
     return checked
 
 
-@pytest.mark.parametrize("n,q,word_bits,batch", [(4096, Q31, 32, 65536), (1024, Q31, 32, 4096),
-                                                  (65536, Q62, 64, 1024), (8192, Q31, 32, 2500)])
-def test_full_size_device_path(n, q, word_bits, batch, torch_cuda):
-    """BASELINE configs C3, C2 and C5 at full size on device-resident data (plus n = 8192 over
-    three multi-pass sub-batches): every product against the oracle, bit-exact."""
+@pytest.mark.parametrize("n,q,word_bits,batch,chunk_mb", [
+    (4096, Q31, 32, 65536, None), (1024, Q31, 32, 4096, None), (65536, Q62, 64, 1024, None),
+    (65536, Q62, 64, 1024, 64), (8192, Q31, 32, 2500, 32)])
+def test_full_size_device_path(n, q, word_bits, batch, chunk_mb, torch_cuda, monkeypatch):
+    """BASELINE configs C3, C2 and C5 at full size on device-resident data, C5 also in 8
+    multi-pass sub-batches and n = 8192 in three (NTTMUL_MP_CHUNK_MB): every product against the
+    oracle, bit-exact."""
     torch = torch_cuda
+    if chunk_mb:
+        monkeypatch.setenv("NTTMUL_MP_CHUNK_MB", str(chunk_mb))
     ctx = _ctx(n, q)
     dt = _torch_dtype(torch, word_bits)
     a = torch.empty(batch * n, dtype=dt, device="cuda")
