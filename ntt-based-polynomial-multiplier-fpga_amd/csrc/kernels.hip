@@ -59,6 +59,10 @@
 #ifndef NTTMUL_KBENCH_LITE
 #define NTTMUL_KBENCH_LITE 0
 #endif
+// conflict-free LDS padding for the group 0 <-> 1 exchanges (Groups::padx; 0 = e + (e >> 4))
+#ifndef NTTMUL_PAD0
+#define NTTMUL_PAD0 1
+#endif
 // column stages of the n = 65536 multi-pass product (4: 16 x 4096 rows, 5: 32 x 2048)
 #ifndef NTTMUL_SPLIT16
 #define NTTMUL_SPLIT16 4
@@ -133,8 +137,20 @@ struct Groups {
       if (off(g, k) == o) return k;
     return -1;
   }
-  static constexpr int pad(int e) { return e + (e >> 4); }
-  static constexpr int NP = N + N / 16;  // padded LDS words per polynomial
+  // LDS padding of exchange X (between register groups X and X + 1): e + ((e >> s) << t), linear
+  // over bit-disjoint parts (so pad(base + off) = pad(base) + pad(off) and off stays an
+  // immediate offset).  Chosen per exchange by a bank census of both register layouts it
+  // connects (32 banks per 32-lane group): group 0 hands each lane consecutive
+  // elements across the wave, which e + (e >> 4) 2-way conflicts (every 32 consecutive words span
+  // 34); e + ((e >> (LOGS - 4)) << (LOGS - 8)) keeps those lanes on distinct banks and still
+  // separates group 1's two 16-element halves.  Exchange 1 (groups 1 <-> 2) keeps e + (e >> 4).
+  static constexpr bool kPad0 = NTTMUL_PAD0 && LOGS >= 10 && G > 2;
+  static constexpr int PS(int x) { return x == 0 && kPad0 ? LOGS - 4 : 4; }
+  static constexpr int PT(int x) { return x == 0 && kPad0 ? LOGS - 8 : 0; }
+  template <int X>
+  static constexpr int padx(int e) { return e + ((e >> PS(X)) << PT(X)); }
+  static constexpr int pad(int e) { return padx<1>(e); }
+  static constexpr int NP = N + N / 16;  // padded LDS words per polynomial (>= every padx)
 };
 
 template <class W, class T>
@@ -276,33 +292,34 @@ __device__ __forceinline__ void exchange(W (&x)[16], W (&y)[16], W *lds_x, W *ld
 #if NTTMUL_ABL_NOXCHG
   return;
 #endif
-  const int bw = Gr::pad(Gr::base(gfrom, j));
-  const int br = Gr::pad(Gr::base(gto, j));
+  constexpr int X = gfrom < gto ? gfrom : gto;
+  const int bw = Gr::template padx<X>(Gr::base(gfrom, j));
+  const int br = Gr::template padx<X>(Gr::base(gto, j));
   if (lds_regions<W>() == 1 && NREG == 2) {  // one region, the two polynomials in turn
 #pragma unroll
-    for (int k = 0; k < 16; k++) lds_x[bw + Gr::pad(Gr::off(gfrom, k))] = x[k];
+    for (int k = 0; k < 16; k++) lds_x[bw + Gr::template padx<X>(Gr::off(gfrom, k))] = x[k];
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 16; k++) x[k] = lds_x[br + Gr::pad(Gr::off(gto, k))];
+    for (int k = 0; k < 16; k++) x[k] = lds_x[br + Gr::template padx<X>(Gr::off(gto, k))];
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 16; k++) lds_x[bw + Gr::pad(Gr::off(gfrom, k))] = y[k];
+    for (int k = 0; k < 16; k++) lds_x[bw + Gr::template padx<X>(Gr::off(gfrom, k))] = y[k];
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 16; k++) y[k] = lds_x[br + Gr::pad(Gr::off(gto, k))];
+    for (int k = 0; k < 16; k++) y[k] = lds_x[br + Gr::template padx<X>(Gr::off(gto, k))];
     __syncthreads();
     return;
   }
 #pragma unroll
   for (int k = 0; k < 16; k++) {
-    lds_x[bw + Gr::pad(Gr::off(gfrom, k))] = x[k];
-    if (NREG == 2) lds_y[bw + Gr::pad(Gr::off(gfrom, k))] = y[k];
+    lds_x[bw + Gr::template padx<X>(Gr::off(gfrom, k))] = x[k];
+    if (NREG == 2) lds_y[bw + Gr::template padx<X>(Gr::off(gfrom, k))] = y[k];
   }
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < 16; k++) {
-    x[k] = lds_x[br + Gr::pad(Gr::off(gto, k))];
-    if (NREG == 2) y[k] = lds_y[br + Gr::pad(Gr::off(gto, k))];
+    x[k] = lds_x[br + Gr::template padx<X>(Gr::off(gto, k))];
+    if (NREG == 2) y[k] = lds_y[br + Gr::template padx<X>(Gr::off(gto, k))];
   }
   __syncthreads();
 }

@@ -32,6 +32,14 @@
 #ifndef NTTMUL_A32_MONT
 #define NTTMUL_A32_MONT 1
 #endif
+// Arith32 twiddle products as Seiler's signed Montgomery (v_mul_lo + 2 v_mul_hi + v_sub, no
+// carry-out SGPR writes); the planner then stores -w2 (A/B variant, untyped butterflies only)
+#ifndef NTTMUL_A32_SEILER
+#define NTTMUL_A32_SEILER 0
+#endif
+#if NTTMUL_A32_SEILER && NTTMUL_TYPED
+#error "NTTMUL_A32_SEILER needs NTTMUL_TYPED=0"
+#endif
 
 namespace nttmul {
 
@@ -78,7 +86,19 @@ struct Arith32T {
 #endif
   }
 
-#if NTTMUL_A32_MONT
+#if NTTMUL_A32_SEILER
+  // x w 2^-32 in (-q, q) for any 32-bit x: m = x w2n with w2n = w1 q^-1 mod 2^32, so x w1 and
+  // m q agree in their low words and the difference of the high words is exact
+  __device__ __forceinline__ uint32_t mont_sl(uint32_t x, uint32_t w1, uint32_t w2n) const {
+    const uint32_t m = x * w2n;
+    return __umulhi(x, w1) - __umulhi(m, q);
+  }
+  __device__ __forceinline__ uint32_t shoup(uint32_t x, uint32_t w1, uint32_t w2n) const {
+    return mont_sl(x, w1, w2n) + q;  // [0, 2q)
+  }
+  // (-q, q) -> [0, q) without a carry: t + q wraps to the small value exactly when t < 0
+  __device__ __forceinline__ static uint32_t fold(uint32_t t, uint32_t m) { return min(t, t + m); }
+#elif NTTMUL_A32_MONT
   // x * w mod q in [0, 2q) for any 32-bit x, twiddle in Montgomery form (w1 = w 2^32 mod q,
   // w2 = w1 (-q^-1) mod 2^32): (x w1 + m q) / 2^32 with m = x w2 mod 2^32 — one v_mul_lo_u32
   // and two v_mad_u64_u32, no trailing subtraction.  x w1 + m q < 2^33 q < 2^64 for q < 2^31.
@@ -157,7 +177,11 @@ struct Arith32T {
       return;
     }
     uint32_t x = XC ? X : csub(X, q);
+#if NTTMUL_A32_SEILER
+    uint32_t t = fold(mont_sl(Y, w, ws), q);
+#else
     uint32_t t = csub(shoup(Y, w, ws), q);
+#endif
     X = x + t;
     Y = x - t + q;
   }
@@ -220,7 +244,11 @@ struct Arith32T {
       w2 = 0u - w2;
     } else if (NEG) {  // -w in Montgomery form: (q - w1, (q - w1)(-q^-1) = ~w2 mod 2^32)
       w1 = q - w1;
+#if NTTMUL_A32_SEILER
+      w2 = 1u - w2;     // (q - w1) q^-1 = 1 - w1 q^-1
+#else
       w2 = ~w2;
+#endif
     }
     uint32_t ar[B], br[B], bz[B];
 #pragma unroll

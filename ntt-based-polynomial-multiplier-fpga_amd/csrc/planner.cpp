@@ -83,6 +83,9 @@ static void tw_pair(uint64_t w, uint64_t q, int bits, uint64_t *v, uint64_t *c) 
     const uint64_t w1 = (uint64_t)(((u128)w << 32) % q);
     *v = w1;
     *c = (w1 * (0 - inv)) & 0xFFFFFFFFull;
+#if NTTMUL_A32_SEILER
+    if (q < (1ull << 31)) *c = (w1 * inv) & 0xFFFFFFFFull;  // Seiler: w1 q^-1 (modarith.hpp)
+#endif
     return;
   }
   *v = w;

@@ -15,6 +15,9 @@
 #ifndef NTTMUL_A32_MONT
 #define NTTMUL_A32_MONT 1
 #endif
+#ifndef NTTMUL_A32_SEILER  // modarith.hpp: the A/B variant's tables store w1 q^-1 instead
+#define NTTMUL_A32_SEILER 0
+#endif
 
 namespace nttmul {
 
