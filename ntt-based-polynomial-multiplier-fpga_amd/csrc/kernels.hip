@@ -403,17 +403,28 @@ __device__ __forceinline__ void base_mult(const A &ar, typename A::word (&x)[16]
   }
 }
 
+// Threads per k_rows workgroup: 256 (one n = 4096 product, or 256 / (n / 16) smaller ones),
+// except one wave per workgroup at n = 1024 (NTTMUL_SMALL_BLOCK): one product per wave, so no
+// barrier ties four independent products together.  C2 (n = 1024 x 4096) 22.2 -> 21.6 us,
+// n = 1024 x 262144 -1 %; n = 256 one wave per 4 products was not faster (profiles/r2)
+#ifndef NTTMUL_SMALL_BLOCK
+#define NTTMUL_SMALL_BLOCK 1
+#endif
+__host__ __device__ constexpr int rows_threads(int logs) {
+  return NTTMUL_SMALL_BLOCK && logs == 10 ? 64 : 256;
+}
+
 // Fused product of `units` independent rows of 2^LOGS coefficients.
 //   L1 == 0 : each unit is a whole polynomial (n = 2^LOGS): full product, canonical output.
 //   L1 >  0 : unit u is row (u mod 2^L1) of polynomial (u >> L1) after the column pass; the
 //             row's stages are global stages L1 .. L1+LOGS-1; output stays lazy in [0, 2q).
 template <class A, class TIn, class TOut, int LOGS, int L1>
-__global__ __launch_bounds__(256, NTTMUL_MIN_WAVES) void k_rows(KParams<A> P, const TIn *__restrict__ a,
-                                              const TIn *__restrict__ b, TOut *__restrict__ c,
-                                              size_t units) {
+__global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
+    KParams<A> P, const TIn *__restrict__ a, const TIn *__restrict__ b, TOut *__restrict__ c,
+    size_t units) {
   using W = typename A::word;
   using Gr = Groups<LOGS>;
-  constexpr int N = Gr::N, TP = N / 16, PB = 256 / TP, G = Gr::G, NP = Gr::NP;
+  constexpr int N = Gr::N, TP = N / 16, PB = rows_threads(LOGS) / TP, G = Gr::G, NP = Gr::NP;
   __shared__ W lds[PB][lds_regions<W>()][NP];
 
   const int pb = threadIdx.x / TP, j = threadIdx.x % TP;
@@ -669,10 +680,10 @@ static KParams<A> product_params(const LaunchTables &T) {
 template <class A, class TIn, class TOut, int LOGS, int L1>
 static hipError_t launch_rows(const KParams<A> &P, const void *a, const void *b, void *c,
                               size_t units, hipStream_t s) {
-  constexpr int PB = 256 / ((1 << LOGS) / 16);
+  constexpr int NT = rows_threads(LOGS), PB = NT / ((1 << LOGS) / 16);
   const size_t blocks = (units + PB - 1) / PB;
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((k_rows<A, TIn, TOut, LOGS, L1>), dim3((unsigned)blocks), dim3(256), 0, s, P,
+  hipLaunchKernelGGL((k_rows<A, TIn, TOut, LOGS, L1>), dim3((unsigned)blocks), dim3(NT), 0, s, P,
                      (const TIn *)a, (const TIn *)b, (TOut *)c, units);
   return hipGetLastError();
 }

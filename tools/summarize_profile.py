@@ -42,14 +42,16 @@ cfg = bench["config"]
 entry_co = bench.get("build", {}).get("code_object")
 main = "k_rows" if "k_rows" in out else sorted(out)[0]
 m = out[main]
-fetch = 2.0 * m["FETCH_SIZE"] * 1024
-write = m["WRITE_SIZE"] * 1024
+# one step = one dispatch of each product kernel (k_rows; plus k_cols_fwd/k_cols_inv for n > 4096)
+step_kernels = sorted(k for k in out if k.startswith(("k_rows", "k_cols")))
+fetch = sum(2.0 * out[k].get("FETCH_SIZE", 0.0) * 1024 for k in step_kernels)
+write = sum(out[k].get("WRITE_SIZE", 0.0) * 1024 for k in step_kernels)
 tpath = os.path.join(os.path.dirname(dst) or ".", "pmc_traffic.json")
 table = json.load(open(tpath)) if os.path.exists(tpath) else {"entries": []}
 table["entries"] = [e for e in table["entries"]
                     if not (e["n"] == cfg["n"] and e["q"] == cfg["q"] and e["batch"] == cfg["batch_per_gpu"]
                             and e.get("code_object") == entry_co)]
-entry = {"n": cfg["n"], "q": cfg["q"], "batch": cfg["batch_per_gpu"], "kernel": main,
+entry = {"n": cfg["n"], "q": cfg["q"], "batch": cfg["batch_per_gpu"], "kernel": "+".join(step_kernels),
          "code_object": bench.get("build", {}).get("code_object"),
          "hbm_bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
          "alg_bytes_per_launch": bench["roofline"]["alg_bytes_per_launch"],
