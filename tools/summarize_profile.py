@@ -46,7 +46,7 @@ m = out[main]
 step_kernels = sorted(k for k in out if k.startswith(("k_rows", "k_cols")))
 fetch = sum(2.0 * out[k].get("FETCH_SIZE", 0.0) * 1024 for k in step_kernels)
 write = sum(out[k].get("WRITE_SIZE", 0.0) * 1024 for k in step_kernels)
-tpath = os.path.join(os.path.dirname(dst) or ".", "pmc_traffic.json")
+tpath = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_traffic.json")
 table = json.load(open(tpath)) if os.path.exists(tpath) else {"entries": []}
 table["entries"] = [e for e in table["entries"]
                     if not (e["n"] == cfg["n"] and e["q"] == cfg["q"] and e["batch"] == cfg["batch_per_gpu"]
