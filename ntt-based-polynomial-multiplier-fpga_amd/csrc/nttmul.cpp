@@ -49,11 +49,22 @@ struct Scratch {
   hipStream_t last = nullptr;                 // stream of that use
 };
 
+// One lane of the pipelined multi-pass product: an internal stream and its own scratch.
+// Sub-batches alternate over kLanes lanes, so one sub-batch's HBM-bound column passes run beside
+// another's VALU-bound row pass.
+constexpr int kLanes = 2;
+struct Lane {
+  hipStream_t s = nullptr;
+  Scratch sc;
+};
+
 struct DevState {
   int id = -1;
   hipStream_t stream = nullptr;
   void *fw = nullptr, *iw = nullptr;
   Scratch dscr;                               // device-resident API calls
+  Lane lane[kLanes];                          // pipelined multi-pass products
+  hipEvent_t lanes_in = nullptr;              // the caller's stream reached the product
   // host-buffer path: kSlots pipeline slots, each with a stream, pinned host staging, device
   // buffers for a, b, c and its own scratch (run_host)
   hipStream_t xs[kSlots] = {};
@@ -140,10 +151,14 @@ int ensure(nttmul_ctx *ctx, Scratch &sc, void **bufs, int nb, size_t *have, size
 // 8/16/32/64/128 MiB ran 2.86/1.91/1.60/1.48/1.40 ms against 1.36 ms in one pass
 // (gpurun_out/r2a) — each sub-batch launch is a single generation of blocks.  The
 // bound also caps scratch memory for very large batches.
-size_t sub_batch(size_t poly_bytes, size_t batch) {
-  const char *e = getenv("NTTMUL_MP_CHUNK_MB");
-  const long v = e ? atol(e) : 512;
-  const size_t mb = v > 0 ? (size_t)v : 512;
+size_t env_size(const char *name, size_t dflt) {
+  const char *e = getenv(name);
+  const long v = e ? atol(e) : 0;
+  return v > 0 ? (size_t)v : dflt;
+}
+
+size_t sub_batch(size_t poly_bytes, size_t batch, size_t dflt_mb = 512) {
+  const size_t mb = env_size("NTTMUL_MP_CHUNK_MB", dflt_mb);
   return std::max<size_t>(1, std::min(batch, (mb << 20) / poly_bytes));
 }
 
@@ -177,6 +192,47 @@ enum Op {
   OP_INVERSE = OP_XFORM + (NTTMUL_XF_INVERSE | NTTMUL_XF_REV2STD),
 };
 constexpr unsigned kXfModes = NTTMUL_XF_INVERSE | NTTMUL_XF_REV2STD | NTTMUL_XF_UNSCALED;
+
+// Pipelined multi-pass product (n > 4096): sub-batches of `chunk` products alternate over the
+// device's lanes (internal streams, each with its own scratch), all ordered after the caller's
+// stream s and joined back into it, so sub-batch i's row pass (VALU-bound) overlaps sub-batch
+// i + 1's column passes (HBM-bound) and the lanes' intermediates stay in the Infinity Cache.
+constexpr size_t kPipeChunkMB = 64;
+int run_lanes(nttmul_ctx *ctx, DevState &d, const LaunchTables &T, const void *a, const void *b,
+              void *c, size_t batch, size_t chunk, int io_bits, hipStream_t s) {
+  const Plan &P = ctx->plan;
+  const size_t io_poly = (size_t)P.n * (io_bits / 8), w_poly = (size_t)P.n * (P.word_bits / 8);
+  if (!d.lanes_in) HIP_TRY(ctx, hipEventCreateWithFlags(&d.lanes_in, hipEventDisableTiming));
+  HIP_TRY(ctx, hipEventRecord(d.lanes_in, s));
+  const int nl = (int)std::min<size_t>(kLanes, (batch + chunk - 1) / chunk);
+  for (int k = 0; k < nl; k++) {
+    Lane &L = d.lane[k];
+    if (!L.s) HIP_TRY(ctx, hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking));
+    HIP_TRY(ctx, hipStreamWaitEvent(L.s, d.lanes_in, 0));
+    int st = scratch_acquire(ctx, L.sc, L.s);
+    if (!st) st = ensure(ctx, L.sc, L.sc.buf, 3, &L.sc.bytes, chunk * w_poly);
+    if (st) return st;
+  }
+  int st = NTTMUL_OK;
+  size_t i = 0;
+  for (size_t p = 0; p < batch && !st; p += chunk, i++) {
+    Lane &L = d.lane[i % nl];
+    const size_t cnt = std::min(chunk, batch - p);
+    hipError_t e = launch_polymul(T, (const char *)a + p * io_poly, (const char *)b + p * io_poly,
+                                  (char *)c + p * io_poly, cnt, io_bits, L.sc.buf, L.s);
+    if (e != hipSuccess) st = fail(ctx, e, "pipelined sub-batch launch");
+  }
+  for (int k = 0; k < nl; k++) {  // join: s continues after every lane's last sub-batch
+    Lane &L = d.lane[k];
+    const int r = scratch_release(ctx, L.sc, L.s);
+    if (!st) st = r;
+    if (!r) {
+      const hipError_t e = hipStreamWaitEvent(s, L.sc.ev, 0);
+      if (e != hipSuccess && !st) st = fail(ctx, e, "hipStreamWaitEvent");
+    }
+  }
+  return st;
+}
 
 // Enqueue one device-resident batch of `op` on d (current device must be d.id), using scratch sc
 // where the op needs it.  b is unused by the transforms.
@@ -223,7 +279,11 @@ int run_device(nttmul_ctx *ctx, DevState &d, Scratch &sc, int op, void *c, const
     else HIP_TRY(ctx, launch_xform(T, a, c, batch, io_bits, inv, sc.buf, s));
     return NTTMUL_OK;
   }
-  // sub-batches through the scratch (1024 products of 512 KiB in 16 sub-batches)
+  if (multipass && op == OP_MULTIPLY && env_size("NTTMUL_MP_LANES", kLanes) > 1) {
+    const size_t chunk = sub_batch(w_poly, batch, kPipeChunkMB);
+    if (chunk < batch) return run_lanes(ctx, d, T, a, b, c, batch, chunk, io_bits, s);
+  }
+  // sub-batches through the scratch
   const size_t chunk = sub_batch(multipass ? w_poly : io_poly, batch);
   int st = scratch_acquire(ctx, sc, s);
   if (st) return st;
@@ -522,6 +582,11 @@ void nttmul_destroy(nttmul_ctx *ctx) {
       if (d.xs[k]) (void)hipStreamDestroy(d.xs[k]);
     }
     scratch_free(d.dscr);
+    for (Lane &L : d.lane) {
+      scratch_free(L.sc);
+      if (L.s) (void)hipStreamDestroy(L.s);
+    }
+    if (d.lanes_in) (void)hipEventDestroy(d.lanes_in);
     for (void *p : {d.fw, d.iw, (void *)d.flag})
       if (p) (void)hipFree(p);
     if (d.stream) (void)hipStreamDestroy(d.stream);

@@ -230,9 +230,10 @@ def test_c4_last_rank_slice(torch_cuda):
 
 def test_device_calls_on_two_streams(torch_cuda):
     """Two multi-pass products enqueued back to back on two different streams share the
-    context's scratch (nttmul.cpp Scratch): the second waits for the first's sub-batches."""
+    context's pipeline lanes and scratch (nttmul.cpp run_lanes, Scratch): each call's two
+    sub-batches run on the internal lanes after its own stream and join back into it."""
     torch = torch_cuda
-    n, q, batch = 16384, Q31, 200
+    n, q, batch = 16384, Q31, 1200
     ctx = _ctx(n, q)
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
     a = torch.empty(batch * n, dtype=torch.int32, device="cuda")
