@@ -193,10 +193,13 @@ enum Op {
 };
 constexpr unsigned kXfModes = NTTMUL_XF_INVERSE | NTTMUL_XF_REV2STD | NTTMUL_XF_UNSCALED;
 
-// Pipelined multi-pass product (n > 4096): sub-batches of `chunk` products alternate over the
-// device's lanes (internal streams, each with its own scratch), all ordered after the caller's
-// stream s and joined back into it, so sub-batch i's row pass (VALU-bound) overlaps sub-batch
-// i + 1's column passes (HBM-bound) and the lanes' intermediates stay in the Infinity Cache.
+// Pipelined multi-pass product (n > 4096, NTTMUL_MP_LANES=2): sub-batches of `chunk` products
+// alternate over the device's lanes (internal streams, each with its own scratch), all ordered
+// after the caller's stream s and joined back into it, so sub-batch i's row pass can overlap
+// sub-batch i + 1's column passes with the lanes' intermediates in the Infinity Cache.  Measured
+// at C5 (profiles/r2/r2_c5_lanes_ab.txt): 1.402-1.427 ms against 1.414-1.425 ms in one pass —
+// the column passes carry a quarter of the butterflies, so the kernels compete for the same VALU
+// and the overlap buys nothing; off by default.
 constexpr size_t kPipeChunkMB = 64;
 int run_lanes(nttmul_ctx *ctx, DevState &d, const LaunchTables &T, const void *a, const void *b,
               void *c, size_t batch, size_t chunk, int io_bits, hipStream_t s) {
@@ -279,7 +282,7 @@ int run_device(nttmul_ctx *ctx, DevState &d, Scratch &sc, int op, void *c, const
     else HIP_TRY(ctx, launch_xform(T, a, c, batch, io_bits, inv, sc.buf, s));
     return NTTMUL_OK;
   }
-  if (multipass && op == OP_MULTIPLY && env_size("NTTMUL_MP_LANES", kLanes) > 1) {
+  if (multipass && op == OP_MULTIPLY && env_size("NTTMUL_MP_LANES", 1) > 1) {
     const size_t chunk = sub_batch(w_poly, batch, kPipeChunkMB);
     if (chunk < batch) return run_lanes(ctx, d, T, a, b, c, batch, chunk, io_bits, s);
   }

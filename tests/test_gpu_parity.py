@@ -185,16 +185,19 @@ def _check_whole_batch(n, q, word_bits, p0, count, a, b, c, chunk=8192):
     return checked
 
 
-@pytest.mark.parametrize("n,q,word_bits,batch,chunk_mb", [
-    (4096, Q31, 32, 65536, None), (1024, Q31, 32, 4096, None), (65536, Q62, 64, 1024, None),
-    (65536, Q62, 64, 1024, 64), (8192, Q31, 32, 2500, 32)])
-def test_full_size_device_path(n, q, word_bits, batch, chunk_mb, torch_cuda, monkeypatch):
+@pytest.mark.parametrize("n,q,word_bits,batch,chunk_mb,lanes", [
+    (4096, Q31, 32, 65536, None, None), (1024, Q31, 32, 4096, None, None),
+    (65536, Q62, 64, 1024, None, None), (65536, Q62, 64, 1024, 64, 2),
+    (8192, Q31, 32, 2500, 32, None)])
+def test_full_size_device_path(n, q, word_bits, batch, chunk_mb, lanes, torch_cuda, monkeypatch):
     """BASELINE configs C3, C2 and C5 at full size on device-resident data, C5 also in 8
-    multi-pass sub-batches and n = 8192 in three (NTTMUL_MP_CHUNK_MB): every product against the
-    oracle, bit-exact."""
+    multi-pass sub-batches over the two pipeline lanes and n = 8192 in three serial sub-batches
+    (NTTMUL_MP_CHUNK_MB / NTTMUL_MP_LANES): every product against the oracle, bit-exact."""
     torch = torch_cuda
     if chunk_mb:
         monkeypatch.setenv("NTTMUL_MP_CHUNK_MB", str(chunk_mb))
+    if lanes:
+        monkeypatch.setenv("NTTMUL_MP_LANES", str(lanes))
     ctx = _ctx(n, q)
     dt = _torch_dtype(torch, word_bits)
     a = torch.empty(batch * n, dtype=dt, device="cuda")
@@ -228,11 +231,14 @@ def test_c4_last_rank_slice(torch_cuda):
     assert _check_whole_batch(n, q, 32, p0, count, a, b, c) == count
 
 
-def test_device_calls_on_two_streams(torch_cuda):
+@pytest.mark.parametrize("lanes", [1, 2])
+def test_device_calls_on_two_streams(lanes, torch_cuda, monkeypatch):
     """Two multi-pass products enqueued back to back on two different streams share the
-    context's pipeline lanes and scratch (nttmul.cpp run_lanes, Scratch): each call's two
-    sub-batches run on the internal lanes after its own stream and join back into it."""
+    context's scratch (nttmul.cpp Scratch, event-ordered) or, with NTTMUL_MP_LANES=2, its
+    pipeline lanes (run_lanes: each call's two sub-batches run after its own stream and join
+    back into it)."""
     torch = torch_cuda
+    monkeypatch.setenv("NTTMUL_MP_LANES", str(lanes))
     n, q, batch = 16384, Q31, 1200
     ctx = _ctx(n, q)
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
