@@ -69,6 +69,7 @@ struct DevState {
   // buffers for a, b, c and its own scratch (run_host)
   hipStream_t xs[kSlots] = {};
   void *pin[kSlots][3] = {};
+  void *pin_dev[kSlots][3] = {};              // the same pinned buffers as device pointers
   void *dbuf[kSlots][3] = {};
   Scratch sscr[kSlots];
   size_t slot_bytes = 0;
@@ -393,13 +394,14 @@ int ensure_slots(nttmul_ctx *ctx, DevState &d, size_t bytes) {
     for (int k = 0; k < 3; k++) {
       if (d.pin[s][k]) (void)hipHostFree(d.pin[s][k]);
       if (d.dbuf[s][k]) (void)hipFree(d.dbuf[s][k]);
-      d.pin[s][k] = d.dbuf[s][k] = nullptr;
+      d.pin[s][k] = d.pin_dev[s][k] = d.dbuf[s][k] = nullptr;
     }
   }
   d.slot_bytes = 0;
   for (int s = 0; s < kSlots; s++)
     for (int k = 0; k < 3; k++) {
       HIP_TRY(ctx, hipHostMalloc(&d.pin[s][k], bytes, hipHostMallocDefault));
+      HIP_TRY(ctx, hipHostGetDevicePointer(&d.pin_dev[s][k], d.pin[s][k], 0));
       HIP_TRY(ctx, hipMalloc(&d.dbuf[s][k], bytes));
     }
   d.slot_bytes = bytes;
@@ -419,6 +421,10 @@ int run_host(nttmul_ctx *ctx, int op, void *c, const void *a, const void *b, siz
   DeviceGuard guard;
   const size_t pbytes = (size_t)ctx->plan.n * (io_bits / 8);
   const size_t chunk = std::max<size_t>(1, kChunkBytes / pbytes);
+  // per-operand bytes up to which a chunk runs zero-copy on the pinned staging buffers
+  // (NTTMUL_ZEROCOPY_KB, default 64; 0 never)
+  const char *zc_env = getenv("NTTMUL_ZEROCOPY_KB");
+  const size_t zero_copy = (zc_env ? (size_t)atol(zc_env) : 64) << 10;
   struct Pending {
     bool busy = false;
     size_t off = 0, bytes = 0;
@@ -464,6 +470,16 @@ int run_host(nttmul_ctx *ctx, int op, void *c, const void *a, const void *b, siz
       const size_t off = J.next * pbytes, bytes = cnt * pbytes;
       pcopy(d.pin[s][0], (const char *)a + off, bytes);
       if (two) pcopy(d.pin[s][1], (const char *)b + off, bytes);
+      if (bytes <= zero_copy && ctx->plan.logn <= 12) {
+        // small transaction (the ntt256_product* shims): the kernel reads a, b from and writes
+        // c to the pinned staging buffers over PCIe — no copy-engine round trips
+        if ((st = run_device(ctx, d, d.sscr[s], op, d.pin_dev[s][2], d.pin_dev[s][0],
+                             d.pin_dev[s][1], cnt, io_bits, d.xs[s])))
+          break;
+        J.slot[s] = Pending{true, off, bytes};
+        J.next += cnt;
+        continue;
+      }
       hipError_t e = hipMemcpyAsync(d.dbuf[s][0], d.pin[s][0], bytes, hipMemcpyHostToDevice, d.xs[s]);
       if (e == hipSuccess && two)
         e = hipMemcpyAsync(d.dbuf[s][1], d.pin[s][1], bytes, hipMemcpyHostToDevice, d.xs[s]);
