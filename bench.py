@@ -220,6 +220,15 @@ def arith_name(q: int) -> str:
 
 
 IC_BYTES = 256 << 20        # MI355X Infinity Cache (MI355X_MICROARCH.md)
+
+
+def buffer_sets(step_bytes: int, requested: int = 0) -> int:
+    """Distinct (a, b, c) sets the timed steps cycle over: `requested` if given, else enough
+    that a step's working set that fits the Infinity Cache is evicted before it is read again
+    (3 x 256 MiB worth of sets), else 1."""
+    if requested > 0:
+        return requested
+    return -(-3 * IC_BYTES // step_bytes) if step_bytes <= IC_BYTES else 1
 MAX_CLOCK_GHZ = 2.4         # MI355X max engine clock (MI355X_MICROARCH.md)
 SIMDS = 1024                # 256 CUs x 4 SIMDs
 
@@ -252,7 +261,7 @@ def main(argv=None):
     count = p1 - p0
     wbytes = wb // 8
     alg_bytes = 3 * n * wbytes * count                    # read a, b + write c, per launch
-    rotate = args.rotate or (-(-3 * IC_BYTES // alg_bytes) if alg_bytes <= IC_BYTES else 1)
+    rotate = buffer_sets(alg_bytes, args.rotate)
 
     ctx = nttmul.Context(n, q, ndev=1, first_dev=devno)
     dt = torch.int32 if wb == 32 else torch.int64

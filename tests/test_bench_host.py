@@ -1,0 +1,77 @@
+"""Host-side logic of bench.py that the driver's numbers depend on (CPU only): Infinity-Cache
+rotation, the fail-closed profile lookups keyed by code object, the code-object id of the built
+library, and the workload labels."""
+import json
+import os
+import struct
+
+import pytest
+
+import bench
+import nttmul
+
+
+def test_buffer_sets():
+    assert bench.buffer_sets(3 * 4096 * 4 * 65536) == 1            # C3: 3 GiB, HBM anyway
+    c2 = 3 * 1024 * 4 * 4096                                        # C2: 48 MiB
+    assert bench.buffer_sets(c2) == 16 and 16 * c2 >= 3 * bench.IC_BYTES
+    assert bench.buffer_sets(c2, 1) == 1                            # explicit --rotate 1
+    assert bench.buffer_sets(bench.IC_BYTES) == 3
+
+
+def test_workload_names():
+    assert bench.workload_name(4096, 2013265921, 65536, 1) == "C3"
+    assert bench.workload_name(4096, 2013265921, 1 << 20, 8) == "C4"
+    assert bench.workload_name(1024, 2013265921, 4096, 1) == "C2"
+    assert bench.workload_name(65536, 0x3FFFFFFFFFE80001, 1024, 1) == "C5"
+    assert bench.workload_name(2048, 2013265921, 10, 1) == "custom"
+
+
+def _elf_with_fatbin(path, payload: bytes):
+    """A minimal ELF64 with a .shstrtab and a .hip_fatbin section."""
+    names = b"\0.shstrtab\0.hip_fatbin\0"
+    data_off = 64
+    fat_off = data_off + len(names)
+    sh_off = fat_off + len(payload)
+    sh_off += (-sh_off) % 8
+    hdr = bytearray(64)
+    hdr[:4] = b"\x7fELF"
+    hdr[4] = 2                                   # ELFCLASS64
+    hdr[5] = 1
+    struct.pack_into("<Q", hdr, 0x28, sh_off)    # e_shoff
+    struct.pack_into("<HHH", hdr, 0x3A, 64, 3, 1)  # e_shentsize, e_shnum, e_shstrndx
+    secs = bytearray(64 * 3)
+    struct.pack_into("<IIQQQQ", secs, 64, 1, 3, 0, 0, data_off, len(names))     # .shstrtab
+    struct.pack_into("<IIQQQQ", secs, 128, 11, 1, 0, 0, fat_off, len(payload))  # .hip_fatbin
+    body = bytes(hdr) + names + payload
+    body += b"\0" * (sh_off - len(body))
+    with open(path, "wb") as f:
+        f.write(body + bytes(secs))
+
+
+def test_code_object_id(tmp_path):
+    a, b = tmp_path / "a.so", tmp_path / "b.so"
+    _elf_with_fatbin(a, b"kernels v1")
+    _elf_with_fatbin(b, b"kernels v2")
+    ia, ib = nttmul.code_object_id(str(a)), nttmul.code_object_id(str(b))
+    assert len(ia) == 16 and ia != ib
+    assert nttmul.code_object_id(str(a)) == ia                      # deterministic
+    (tmp_path / "x.txt").write_bytes(b"not an elf")
+    with pytest.raises(ValueError):
+        nttmul.code_object_id(str(tmp_path / "x.txt"))
+    if os.path.exists(nttmul.LIB_PATH):                              # the built library has one
+        assert len(nttmul.code_object_id()) == 16
+
+
+def test_profile_lookup_fails_closed(tmp_path, monkeypatch):
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    entry = {"n": 4096, "q": 2013265921, "batch": 65536, "code_object": "aaaa",
+             "hbm_bytes_per_launch": 2.0e9, "source": "x_pmc.json", "method": "m"}
+    (prof / "pmc_traffic.json").write_text(json.dumps({"entries": [entry]}))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    t, src = bench.load_traffic(4096, 2013265921, 32768, "aaaa")
+    assert t == 1.0e9 and "aaaa" in src                            # scaled to the batch
+    t, src = bench.load_traffic(4096, 2013265921, 65536, "bbbb")   # another build
+    assert t is None and "bbbb" in src
+    assert bench.load_valu_bound(4096, 2013265921, "aaaa") is None  # no file: None
