@@ -215,7 +215,7 @@ def arith_name(q: int) -> str:
     if q < (1 << 30):
         return "Arith32H"
     if q < (1 << 31):
-        return "Arith32"
+        return "Arith32P"  # Plantard twiddle products (arith_select.hpp default)
     return "Arith32W" if q < (1 << 32) else "Arith64"
 
 

@@ -34,10 +34,7 @@
 #ifndef NTTMUL_NT
 #define NTTMUL_NT 1
 #endif
-// Arith32H (Harvey bounds) for q < 2^30
-#ifndef NTTMUL_A32H
-#define NTTMUL_A32H 1
-#endif
+// NTTMUL_A32H / NTTMUL_A32_PLANTARD (which 32-bit class takes which q): arith_select.hpp
 // incomplete transforms in the product kernel: the last D = A::kBaseD stages become base
 // multiplications of 2^D-coefficient blocks (0: full transforms + pointwise Montgomery product)
 #ifndef NTTMUL_BASE_D
@@ -467,7 +464,7 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
 #pragma unroll
     for (int k = 0; k < 16; k++) {
       W v = x[k];
-      if (L1 == 0) v = P.ar.canon(v);
+      if (L1 == 0 && !A::kInvCanonical) v = P.ar.canon(v);
       st_stream(c + base_g + Gr::off(0, k), (TOut)v);
     }
   }
@@ -506,7 +503,7 @@ __global__ __launch_bounds__(256) void k_xform(KParams<A> P, const TIn *__restri
 #pragma unroll
     for (int k = 0; k < 16; k++) {
       W v = x[k];
-      if (DIR == 0 || L1 == 0) v = P.ar.canon(v);
+      if (DIR == 0 || (L1 == 0 && !A::kInvCanonical)) v = P.ar.canon(v);
       out[base_out + Gr::off(GOUT, k)] = (TOut)v;
     }
   }
@@ -594,7 +591,8 @@ __global__ __launch_bounds__(256) void k_cols_inv(KParams<A> P,
     }
   }
 #pragma clang loop unroll(full)
-  for (int m = 0; m < M; m++) c[base + ((size_t)m << logs)] = (TOut)P.ar.canon(x[m]);
+  for (int m = 0; m < M; m++)
+    c[base + ((size_t)m << logs)] = (TOut)(A::kInvCanonical ? x[m] : P.ar.canon(x[m]));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -737,40 +735,36 @@ static hipError_t multipass(const LaunchTables &T, const void *a, const void *b,
   }
 }
 
+template <class A>
+static hipError_t polymul_io(const LaunchTables &T, const void *a, const void *b, void *c,
+                             size_t batch, int io_bits, void **scr, hipStream_t s) {
+  const bool big = T.logn > 12;
+  if (io_bits == 64)
+    return big ? multipass<A, uint64_t>(T, a, b, c, batch, scr, s)
+               : fused<A, uint64_t>(T, a, b, c, batch, s);
+  return big ? multipass<A, uint32_t>(T, a, b, c, batch, scr, s)
+             : fused<A, uint32_t>(T, a, b, c, batch, s);
+}
+
 hipError_t launch_polymul(const LaunchTables &T, const void *a, const void *b, void *c,
                           size_t batch, int io_bits, void **scr, hipStream_t s) {
-  const bool big = T.logn > 12;
 #if NTTMUL_KBENCH_LITE  // tools/kbench quick builds: 32-bit words, q < 2^31, n <= 4096 only
   if (T.word_bits != 32 || T.q >= (1ull << 31) || big || io_bits != 32) return hipErrorNotSupported;
-  if (NTTMUL_A32H && T.q < (1ull << 30)) return fused<Arith32H, uint32_t>(T, a, b, c, batch, s);
-  return fused<Arith32, uint32_t>(T, a, b, c, batch, s);
+  switch (a32_kind(T.q)) {
+    case A32Kind::Harvey: return fused<Arith32H, uint32_t>(T, a, b, c, batch, s);
+    case A32Kind::Plantard: return fused<Arith32P, uint32_t>(T, a, b, c, batch, s);
+    default: return fused<Arith32, uint32_t>(T, a, b, c, batch, s);
+  }
 #else
-  if (NTTMUL_A32H && T.word_bits == 32 && T.q < (1ull << 30)) {  // Harvey bounds fit
-    if (io_bits == 64)
-      return big ? multipass<Arith32H, uint64_t>(T, a, b, c, batch, scr, s)
-                 : fused<Arith32H, uint64_t>(T, a, b, c, batch, s);
-    return big ? multipass<Arith32H, uint32_t>(T, a, b, c, batch, scr, s)
-               : fused<Arith32H, uint32_t>(T, a, b, c, batch, s);
+  if (T.word_bits == 32) {  // 64-bit storage of a q < 2^32 product: same 32-bit arithmetic
+    switch (a32_kind(T.q)) {
+      case A32Kind::Harvey: return polymul_io<Arith32H>(T, a, b, c, batch, io_bits, scr, s);
+      case A32Kind::Wide: return polymul_io<Arith32W>(T, a, b, c, batch, io_bits, scr, s);
+      case A32Kind::Plantard: return polymul_io<Arith32P>(T, a, b, c, batch, io_bits, scr, s);
+      case A32Kind::Mont: return polymul_io<Arith32>(T, a, b, c, batch, io_bits, scr, s);
+    }
   }
-  if (T.word_bits == 32 && T.q >= (1ull << 31)) {  // full 32-bit modulus
-    if (io_bits == 64)
-      return big ? multipass<Arith32W, uint64_t>(T, a, b, c, batch, scr, s)
-                 : fused<Arith32W, uint64_t>(T, a, b, c, batch, s);
-    return big ? multipass<Arith32W, uint32_t>(T, a, b, c, batch, scr, s)
-               : fused<Arith32W, uint32_t>(T, a, b, c, batch, s);
-  }
-  if (T.word_bits == 32) {
-    if (io_bits == 64)  // 64-bit storage of a q < 2^31 product: same 32-bit arithmetic
-      return big ? multipass<Arith32, uint64_t>(T, a, b, c, batch, scr, s)
-                 : fused<Arith32, uint64_t>(T, a, b, c, batch, s);
-    return big ? multipass<Arith32, uint32_t>(T, a, b, c, batch, scr, s)
-               : fused<Arith32, uint32_t>(T, a, b, c, batch, s);
-  }
-  if (io_bits == 32)
-    return big ? multipass<Arith64, uint32_t>(T, a, b, c, batch, scr, s)
-               : fused<Arith64, uint32_t>(T, a, b, c, batch, s);
-  return big ? multipass<Arith64, uint64_t>(T, a, b, c, batch, scr, s)
-             : fused<Arith64, uint64_t>(T, a, b, c, batch, s);
+  return polymul_io<Arith64>(T, a, b, c, batch, io_bits, scr, s);
 #endif
 }
 
@@ -844,20 +838,25 @@ static hipError_t xform_any(const LaunchTables &T, const void *in, void *out, si
   }
 }
 
+template <class A, int DIR>
+static hipError_t xform_io(const LaunchTables &T, const void *in, void *out, size_t batch,
+                           int io_bits, void **scr, hipStream_t s) {
+  return io_bits == 64 ? xform_any<A, uint64_t, DIR>(T, in, out, batch, scr, s)
+                       : xform_any<A, uint32_t, DIR>(T, in, out, batch, scr, s);
+}
+
 template <int DIR>
 static hipError_t launch_xform_dir(const LaunchTables &T, const void *in, void *out, size_t batch,
                                    int io_bits, void **scr, hipStream_t s) {
-  if (NTTMUL_A32H && T.word_bits == 32 && T.q < (1ull << 30))
-    return io_bits == 64 ? xform_any<Arith32H, uint64_t, DIR>(T, in, out, batch, scr, s)
-                         : xform_any<Arith32H, uint32_t, DIR>(T, in, out, batch, scr, s);
-  if (T.word_bits == 32 && T.q >= (1ull << 31))
-    return io_bits == 64 ? xform_any<Arith32W, uint64_t, DIR>(T, in, out, batch, scr, s)
-                         : xform_any<Arith32W, uint32_t, DIR>(T, in, out, batch, scr, s);
-  if (T.word_bits == 32)
-    return io_bits == 64 ? xform_any<Arith32, uint64_t, DIR>(T, in, out, batch, scr, s)
-                         : xform_any<Arith32, uint32_t, DIR>(T, in, out, batch, scr, s);
-  return io_bits == 64 ? xform_any<Arith64, uint64_t, DIR>(T, in, out, batch, scr, s)
-                       : xform_any<Arith64, uint32_t, DIR>(T, in, out, batch, scr, s);
+  if (T.word_bits == 32) {
+    switch (a32_kind(T.q)) {
+      case A32Kind::Harvey: return xform_io<Arith32H, DIR>(T, in, out, batch, io_bits, scr, s);
+      case A32Kind::Wide: return xform_io<Arith32W, DIR>(T, in, out, batch, io_bits, scr, s);
+      case A32Kind::Plantard: return xform_io<Arith32P, DIR>(T, in, out, batch, io_bits, scr, s);
+      case A32Kind::Mont: return xform_io<Arith32, DIR>(T, in, out, batch, io_bits, scr, s);
+    }
+  }
+  return xform_io<Arith64, DIR>(T, in, out, batch, io_bits, scr, s);
 }
 
 hipError_t launch_xform(const LaunchTables &T, const void *in, void *out, size_t batch,
@@ -891,7 +890,7 @@ hipError_t launch_pointwise(const LaunchTables &T, const void *a, const void *b,
   if (T.word_bits == 32 && T.q >= (1ull << 31))
     return io_bits == 64 ? pointwise<Arith32W, uint64_t>(T, a, b, c, total, s)
                          : pointwise<Arith32W, uint32_t>(T, a, b, c, total, s);
-  if (T.word_bits == 32)
+  if (T.word_bits == 32)  // Montgomery products only (no twiddle tables): Arith32 for q < 2^31
     return io_bits == 64 ? pointwise<Arith32, uint64_t>(T, a, b, c, total, s)
                          : pointwise<Arith32, uint32_t>(T, a, b, c, total, s);
   return io_bits == 64 ? pointwise<Arith64, uint64_t>(T, a, b, c, total, s)

@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "arith_select.hpp"
+
 // conditional-subtract lowering: 0 = e32 sub_co/cndmask asm, 1 = v_min_u32,
 // 2 = __builtin_sub_overflow + select (default: measured fastest in k_rows, tools/kbench)
 #ifndef NTTMUL_CSUB
@@ -52,6 +54,7 @@ struct Arith32T {
   static constexpr int kBits = 32;
   // typed butterflies (kernels.hip fwd_group / inv_group): see ct_t below
   static constexpr bool kTyped = !H && NTTMUL_TYPED && NTTMUL_A32_MONT;
+  static constexpr bool kInvCanonical = false;  // inverse outputs lazy: canonicalised at the store
   uint32_t q;
   uint32_t qinv_neg;  // -q^-1 mod 2^32
 
@@ -289,6 +292,109 @@ struct Arith32T {
 using Arith32 = Arith32T<false>;   // q < 2^31
 using Arith32H = Arith32T<true>;   // q < 2^30
 
+// q < 2^31 with Plantard twiddle products (T. Plantard, "Efficient word size modular arithmetic",
+// IEEE TETC 2021).  The twiddle w is stored as BR = B q^-1 mod 2^64 with B = -w 2^64 mod q, split
+// (b0, b1) = (low, high) word.  For any 32-bit x:
+//   T = x BR mod 2^64,  t = floor((floor(T / 2^32) + 1) q / 2^32)
+// k = (T q - x B) / 2^64 is an integer in [0, q) congruent to -x B 2^-64 = x w, and
+// t = floor(k + e) with e = (x B + (2^32 - T mod 2^32) q) / 2^64 in (0, 1) whenever
+// x B < 2^32 (2^32 - q), which holds for every 32-bit x and B < q because 2q < 2^32.  So t is
+// the canonical residue of x w, for one v_mul_hi_u32 + v_mul_lo_u32 + v_add_u32 +
+// v_mad_u64_u32 — the same three multiplies as a Montgomery product, whose output spans [0, 2q)
+// and needs a conditional subtraction (two carry/select instructions) before it can be added.
+// Butterflies therefore correct one operand instead of two:
+//   CT  (forward, x lazy in [0, 2q), Y any word): x = csub(X); t = x w; (x + t, x - t + q)
+//   GS  (inverse, x, y canonical): (csub(x + y), (x - y + q) w), both outputs canonical
+// Every inverse value is canonical, so the transform's output needs no final canonicalisation.
+struct Arith32P {
+  using word = uint32_t;
+  static constexpr int kBits = 32;
+  static constexpr bool kTyped = false;
+  static constexpr bool kInvCanonical = true;  // GS outputs are canonical
+  uint32_t q;
+  uint32_t qinv_neg;  // -q^-1 mod 2^32 (Montgomery reduction of the base-multiplication sums)
+
+  __device__ __forceinline__ static uint32_t csub(uint32_t x, uint32_t m) {
+    uint32_t d;
+    return __builtin_sub_overflow(x, m, &d) ? x : d;
+  }
+  // x w mod q in [0, q) for any 32-bit x; (b0, b1) = the planner's Plantard pair of w
+  __device__ __forceinline__ uint32_t pmul(uint32_t x, uint32_t b0, uint32_t b1) const {
+    const uint32_t th = __umulhi(x, b0) + x * b1;
+    return (uint32_t)(((uint64_t)th * q + q) >> 32);
+  }
+  __device__ __forceinline__ uint32_t shoup(uint32_t x, uint32_t b0, uint32_t b1) const {
+    return pmul(x, b0, b1);
+  }
+  // CT (ntt.C:365-367 pattern): X in [0, 2q) (XC: canonical), Y any -> outputs in [0, 2q)
+  template <bool XC = false>
+  __device__ __forceinline__ void ct(uint32_t &X, uint32_t &Y, uint32_t b0, uint32_t b1) const {
+    const uint32_t x = XC ? X : csub(X, q);
+    const uint32_t t = pmul(Y, b0, b1);
+    X = x + t;
+    Y = x - t + q;
+  }
+  // GS (ntt.C:445-447 pattern): X, Y canonical -> outputs canonical
+  __device__ __forceinline__ void gs(uint32_t &X, uint32_t &Y, uint32_t b0, uint32_t b1) const {
+    const uint32_t x = X, y = Y;
+    X = csub(x + y, q);
+    Y = pmul(x - y + q, b0, b1);
+  }
+  // last inverse stage with the output scale F folded in: ((X + Y) F, (X - Y) w F), canonical
+  __device__ __forceinline__ void gs_scaled(uint32_t &X, uint32_t &Y, uint32_t f0, uint32_t f1,
+                                            uint32_t wf0, uint32_t wf1) const {
+    const uint32_t x = X, y = Y;
+    X = pmul(x + y, f0, f1);
+    Y = pmul(x - y + q, wf0, wf1);
+  }
+  // Montgomery a b 2^-32 mod q, a and b in [0, 2q) -> [0, q): a reduced below q, so
+  // a b + m q < 2 q^2 + 2^32 q < 2^64 and the quotient is below 2q
+  __device__ __forceinline__ uint32_t mont(uint32_t a, uint32_t b) const {
+    const uint64_t t = (uint64_t)csub(a, q) * b;
+    const uint32_t m = (uint32_t)t * qinv_neg;
+    return csub((uint32_t)((t + (uint64_t)m * q) >> 32), q);
+  }
+  // [0, 2q) -> [0, q)
+  __device__ __forceinline__ uint32_t canon(uint32_t x) const { return csub(x, q); }
+
+  // Base multiplication (see Arith32T::basemul): a = a b 2^-32 in Z_q[x]/(x^4 - z), z = +-w.
+  // a, b in [0, 2q) from the forward transform; z b_i by Plantard (canonical straight from any
+  // b_i; -w: q - w b_i, in (0, q]); four products per output, each sum below 4 q^2 < 2^64; the
+  // Montgomery quotient (carry c, word hi) is below 2.875 q and is reduced to [0, q) for the
+  // inverse butterflies.
+  static constexpr int kBaseD = 2;
+  template <int B, bool NEG, bool ZC = false>
+  __device__ __forceinline__ void basemul(uint32_t (&a)[B], const uint32_t (&b)[B], uint32_t w0,
+                                          uint32_t w1) const {
+    static_assert(B == 4, "sums of B products must fit 64 bits");
+    uint32_t ar[B], br[B], bz[B];
+#pragma unroll
+    for (int i = 0; i < B; i++) {
+      ar[i] = csub(a[i], q);
+      br[i] = csub(b[i], q);
+    }
+#pragma unroll
+    for (int i = 1; i < B; i++) {
+      const uint32_t t = pmul(b[i], w0, w1);
+      bz[i] = NEG ? q - t : t;
+    }
+#pragma unroll
+    for (int k = 0; k < B; k++) {
+      uint64_t s = 0;
+#pragma unroll
+      for (int i = 0; i < B; i++)
+        s += (uint64_t)ar[i] * (i <= k ? br[k - i] : bz[B + k - i]);
+      const uint32_t m = (uint32_t)s * qinv_neg;
+      uint64_t t;
+      const bool c = __builtin_add_overflow(s, (uint64_t)m * q, &t);  // value c 2^64 + t
+      const uint32_t hi = (uint32_t)(t >> 32);
+      uint32_t d;
+      const bool br2 = __builtin_sub_overflow(hi, 2 * q, &d);
+      a[k] = csub((c || !br2) ? d : hi, q);
+    }
+  }
+};
+
 // 2^31 <= q < 2^32 in 32-bit words: no room above q, so values stay canonical in [0, q) and every
 // sum / difference / product is reduced completely; the 65th bit of a Montgomery sum is the
 // carry of a 64-bit add.  About 14 VALU instructions per butterfly, against ~30 for taking this q
@@ -297,6 +403,7 @@ struct Arith32W {
   using word = uint32_t;
   static constexpr int kBits = 32;
   static constexpr bool kTyped = false;
+  static constexpr bool kInvCanonical = false;
   uint32_t q;
   uint32_t qinv_neg;  // -q^-1 mod 2^32
 
@@ -368,6 +475,7 @@ struct Arith64 {
   using word = uint64_t;
   static constexpr int kBits = 64;
   static constexpr bool kTyped = false;
+  static constexpr bool kInvCanonical = false;
   uint64_t q;
   uint64_t qinv_neg;  // -q^-1 mod 2^64
 

@@ -73,9 +73,21 @@ static uint64_t companion(uint64_t w, uint64_t q, int bits) {
   return (uint64_t)(((u128)w << bits) / q);
 }
 
-// (value, companion) pair the device multiplies by: Shoup (w, floor(w 2^bits / q)), or for
-// Arith32 with NTTMUL_A32_MONT the Montgomery form (w 2^32 mod q, that times -q^-1 mod 2^32)
+// (value, companion) pair the device multiplies by: Shoup (w, floor(w 2^bits / q)); for
+// Arith32P (arith_select.hpp) the Plantard constant BR = B q^-1 mod 2^64, B = -w 2^64 mod q, as
+// (low, high) words; for the other 32-bit classes the Montgomery form (w 2^32 mod q, that times
+// -q^-1 mod 2^32)
 static void tw_pair(uint64_t w, uint64_t q, int bits, uint64_t *v, uint64_t *c) {
+  if (bits == 32 && a32_kind(q) == A32Kind::Plantard) {
+    uint64_t inv = q;  // q^-1 mod 2^64 (Newton on the 2-adic inverse)
+    for (int i = 0; i < 6; i++) inv *= 2 - q * inv;
+    const uint64_t r64 = (uint64_t)(((u128)1 << 64) % q);
+    const uint64_t b = (q - mulmod(w % q, r64, q)) % q;
+    const uint64_t br = b * inv;
+    *v = br & 0xFFFFFFFFull;
+    *c = br >> 32;
+    return;
+  }
   // Arith32W (q >= 2^31) always takes the Montgomery form
   if (bits == 32 && (NTTMUL_A32_MONT || q >= (1ull << 31))) {
     uint64_t inv = q;
@@ -201,7 +213,7 @@ int make_plan(uint32_t n, uint64_t q, uint64_t psi, Plan *P, bool cyclic) {
   if (bits == 32) {
     put_pairs<uint32_t>(P->fw, fw, q, 32);
     put_pairs<uint32_t>(P->iw, iw, q, 32);
-    if (NTTMUL_A32_MONT && q < (1ull << 31)) {  // Arith32 typed butterflies: centred copies
+    if (NTTMUL_A32_MONT && a32_kind(q) == A32Kind::Mont) {  // typed butterflies: centred copies
       append_centred(P->fw, n, q);
       append_centred(P->iw, n, q);
     }

@@ -11,6 +11,8 @@
 
 #include <vector>
 
+#include "arith_select.hpp"
+
 // Arith32 twiddle form (see modarith.hpp); host tables and device kernels must agree
 #ifndef NTTMUL_A32_MONT
 #define NTTMUL_A32_MONT 1
