@@ -21,14 +21,17 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "launch.hpp"
 #include "modarith.hpp"
 
 // LDS regions per polynomial pair for 32-bit words (2: a and b exchanged together; 1: in turn,
-// half the LDS).  64-bit words always use one region: two would be 68 KiB per block, 2 blocks per
-// CU; one region lets 3-4 blocks share a CU (C5 -6 %, tools/c5_ab.sh)
+// half the LDS).  One region: 17 KiB per n = 4096 block, 7 blocks (VGPR-limited) instead of 4 per
+// CU; with the Plantard kernel -2 % at C3, -1 % at n = 1024 x 262144 and n = 65536, C2 unchanged
+// (profiles/r2/plantard/ab1.txt).  64-bit words always use one region (C5 -6 %, tools/c5_ab.sh)
 #ifndef NTTMUL_LDS_REGIONS
-#define NTTMUL_LDS_REGIONS 2
+#define NTTMUL_LDS_REGIONS 1
 #endif
 // non-temporal loads/stores of the coefficient streams in k_rows
 #ifndef NTTMUL_NT
@@ -153,6 +156,17 @@ struct Groups {
 template <class W, class T>
 __device__ __forceinline__ W to_word(T v) { return (W)v; }
 
+// Arith32P's typed CT (modarith.hpp Arith32P::ct<XC, XN, YN>)
+template <class A>
+struct IsPlantard : std::false_type {};
+template <>
+struct IsPlantard<Arith32P> : std::true_type {};
+template <class A>
+__host__ __device__ constexpr bool kTypedP() {
+  if constexpr (IsPlantard<A>::value) return A::kTypedP;
+  return false;
+}
+
 // Coefficient streams are touched once per product: NTTMUL_NT marks them non-temporal
 template <class T>
 __device__ __forceinline__ T ld_stream(const T *p) {
@@ -217,6 +231,28 @@ __device__ __forceinline__ void fwd_group(const A &ar, typename A::word (&x)[16]
       }
       const TwPair<typename A::word> t = tw[NTTMUL_ABL_TWMASK ? (idx & NTTMUL_ABL_TWMASK) : idx];
       if (l == S - SKIP - 1) zw[k] = t;
+      if constexpr (kTypedP<A>()) {
+        // Arith32P: register k was written as a (signed) difference by the previous stage iff
+        // bit 2 dist is set; this stage leaves its difference in k + dist signed iff the next
+        // stage of the group uses that register as an X (bit dist / 2 clear)
+        const bool xn = l > 0 && (k & (2 * dist));
+        const bool yn = l < S - SKIP - 1 && !((k + dist) & (dist >> 1));
+        const bool xc = NTTMUL_FIRST_XC && g == 0 && l == 0 && l1 == 0;
+#define NTTMUL_CT_P(XC_, XN_, YN_)                                         \
+  do {                                                                     \
+    ar.template ct<XC_, XN_, YN_>(x[k], x[k + dist], t.w, t.ws);            \
+    if (NPOLY == 2) ar.template ct<XC_, XN_, YN_>(y[k], y[k + dist], t.w, t.ws); \
+  } while (0)
+        if (xc) {
+          if (yn) NTTMUL_CT_P(true, false, true); else NTTMUL_CT_P(true, false, false);
+        } else if (xn) {
+          if (yn) NTTMUL_CT_P(false, true, true); else NTTMUL_CT_P(false, true, false);
+        } else {
+          if (yn) NTTMUL_CT_P(false, false, true); else NTTMUL_CT_P(false, false, false);
+        }
+#undef NTTMUL_CT_P
+        continue;
+      }
       // global stage 0 of a whole polynomial reads canonical input (the API contract, [0, q)):
       // its X operands need no reduction
       if (NTTMUL_FIRST_XC && g == 0 && l == 0 && l1 == 0) {
@@ -656,6 +692,7 @@ static KParams<A> make_params(const LaunchTables &T) {
   KParams<A> P;
   P.ar.q = (W)T.q;
   P.ar.qinv_neg = (W)T.qinv_neg;
+  if constexpr (IsPlantard<A>::value) P.ar.c32 = (uint32_t)((1ull << 32) % T.q);
   P.fw = (const TwPair<W> *)T.fw;
   P.iw = (const TwPair<W> *)T.iw;
   P.f = (W)T.f; P.fs = (W)T.fs; P.wf = (W)T.wf; P.wfs = (W)T.wfs;

@@ -306,13 +306,24 @@ using Arith32H = Arith32T<true>;   // q < 2^30
 //   CT  (forward, x lazy in [0, 2q), Y any word): x = csub(X); t = x w; (x + t, x - t + q)
 //   GS  (inverse, x, y canonical): (csub(x + y), (x - y + q) w), both outputs canonical
 // Every inverse value is canonical, so the transform's output needs no final canonicalisation.
+#ifndef NTTMUL_P_TYPED  // Arith32P: CT differences that feed an addition stay signed (no "+ q")
+#define NTTMUL_P_TYPED 1
+#endif
+#ifndef NTTMUL_P_HI  // Arith32P: last Plantard step as v_mul_hi_u32(th + 1, q) (A/B variant)
+#define NTTMUL_P_HI 0
+#endif
+#ifndef NTTMUL_P_FOLD  // Arith32P base multiplication: fold the sum's high word by 2^32 mod q
+#define NTTMUL_P_FOLD 1
+#endif
 struct Arith32P {
   using word = uint32_t;
   static constexpr int kBits = 32;
   static constexpr bool kTyped = false;
+  static constexpr bool kTypedP = NTTMUL_P_TYPED;  // kernels.hip fwd_group: ct<XC, XN, YN>
   static constexpr bool kInvCanonical = true;  // GS outputs are canonical
   uint32_t q;
   uint32_t qinv_neg;  // -q^-1 mod 2^32 (Montgomery reduction of the base-multiplication sums)
+  uint32_t c32;       // 2^32 mod q
 
   __device__ __forceinline__ static uint32_t csub(uint32_t x, uint32_t m) {
     uint32_t d;
@@ -321,18 +332,33 @@ struct Arith32P {
   // x w mod q in [0, q) for any 32-bit x; (b0, b1) = the planner's Plantard pair of w
   __device__ __forceinline__ uint32_t pmul(uint32_t x, uint32_t b0, uint32_t b1) const {
     const uint32_t th = __umulhi(x, b0) + x * b1;
+#if NTTMUL_P_HI
+    // th + 1 never wraps: th = 2^32 - 1 would give t = q, and t < q
+    return __umulhi(th + 1, q);
+#else
     return (uint32_t)(((uint64_t)th * q + q) >> 32);
+#endif
   }
   __device__ __forceinline__ uint32_t shoup(uint32_t x, uint32_t b0, uint32_t b1) const {
     return pmul(x, b0, b1);
   }
-  // CT (ntt.C:365-367 pattern): X in [0, 2q) (XC: canonical), Y any -> outputs in [0, 2q)
-  template <bool XC = false>
+  // CT (ntt.C:365-367 pattern): X in [0, 2q) (XC: canonical; XN: signed in (-q, q)), Y any ->
+  // X' in [0, 2q), Y' in (0, 2q) (YN: x - t signed in (-q, q), for a register whose next use is
+  // as the X of a butterfly, where the carry of x + q corrects it as cheaply as csub would)
+  template <bool XC = false, bool XN = false, bool YN = false>
   __device__ __forceinline__ void ct(uint32_t &X, uint32_t &Y, uint32_t b0, uint32_t b1) const {
-    const uint32_t x = XC ? X : csub(X, q);
+    uint32_t x;
+    if (XC) {
+      x = X;
+    } else if (XN) {
+      uint32_t e;
+      x = __builtin_add_overflow(X, q, &e) ? e : X;
+    } else {
+      x = csub(X, q);
+    }
     const uint32_t t = pmul(Y, b0, b1);
     X = x + t;
-    Y = x - t + q;
+    Y = YN ? x - t : x - t + q;
   }
   // GS (ntt.C:445-447 pattern): X, Y canonical -> outputs canonical
   __device__ __forceinline__ void gs(uint32_t &X, uint32_t &Y, uint32_t b0, uint32_t b1) const {
@@ -384,6 +410,13 @@ struct Arith32P {
 #pragma unroll
       for (int i = 0; i < B; i++)
         s += (uint64_t)ar[i] * (i <= k ? br[k - i] : bz[B + k - i]);
+#if NTTMUL_P_FOLD
+      // s = h 2^32 + l == h c32 + l (mod q): s2 <= 4 (q-1)^3 / 2^32 + 2^32 - 1, so s2 + m q < 2^64
+      // and the Montgomery quotient is below (q - 1) + 1 + q = 2q: one csub to canonical
+      const uint64_t s2 = (uint64_t)(uint32_t)(s >> 32) * c32 + (uint32_t)s;
+      const uint32_t m = (uint32_t)s2 * qinv_neg;
+      a[k] = csub((uint32_t)((s2 + (uint64_t)m * q) >> 32), q);
+#else
       const uint32_t m = (uint32_t)s * qinv_neg;
       uint64_t t;
       const bool c = __builtin_add_overflow(s, (uint64_t)m * q, &t);  // value c 2^64 + t
@@ -391,6 +424,7 @@ struct Arith32P {
       uint32_t d;
       const bool br2 = __builtin_sub_overflow(hi, 2 * q, &d);
       a[k] = csub((c || !br2) ? d : hi, q);
+#endif
     }
   }
 };

@@ -14,8 +14,8 @@ step() {  # name, timeout, command...: stop the session at the first failure
   if [ $rc -ne 0 ]; then echo "FAILED $name rc=$rc" >&2; tail -40 $OUT/$name.log >&2; exit $rc; fi
   tail -4 $OUT/$name.log >&2
 }
-step ab_c3 200 tools/kbench/ab3.sh 4096 2013265921 65536 100
-step ab_n1024 200 tools/kbench/ab3.sh 1024 2013265921 262144 100
+export VARIANTS="base prev nofold notyped lds1 compute"; step ab_c3 300 tools/kbench/ab3.sh 4096 2013265921 65536 100
+export VARIANTS="base prev"; step ab_n1024 200 tools/kbench/ab3.sh 1024 2013265921 262144 100
 if [ "$2" != "skip-tests" ]; then
   step gpu_tests 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
 fi
