@@ -14,6 +14,12 @@
 #define NTTMUL_A32_PLANTARD 1
 #endif
 
+// Arith32P inverse twiddles in the signed-input Plantard form (the GS difference x - y in (-q, q)
+// is multiplied without "+ q"); planner and kernels must agree
+#ifndef NTTMUL_P_SIGNED_INV
+#define NTTMUL_P_SIGNED_INV 1
+#endif
+
 namespace nttmul {
 
 enum class A32Kind { Harvey, Plantard, Mont, Wide };

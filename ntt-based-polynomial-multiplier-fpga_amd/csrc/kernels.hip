@@ -167,22 +167,24 @@ __host__ __device__ constexpr bool kTypedP() {
   return false;
 }
 
-// Coefficient streams are touched once per product: NTTMUL_NT marks them non-temporal
-template <class T>
+// Coefficient streams are touched once per product: NTTMUL_NT marks them non-temporal.  The row
+// pass of a multi-pass product (L1 > 0) reads and writes intermediates that the column passes
+// touch again, so NTTMUL_NT_MP (default 0) keeps those accesses temporal: a sub-batch whose
+// scratch fits the Infinity Cache can then stay there between the three launches.
+#ifndef NTTMUL_NT_MP
+#define NTTMUL_NT_MP 0
+#endif
+template <bool NT, class T>
 __device__ __forceinline__ T ld_stream(const T *p) {
-#if NTTMUL_NT
-  return __builtin_nontemporal_load(p);
-#else
+  if constexpr (NT) return __builtin_nontemporal_load(p);
   return *p;
-#endif
 }
-template <class T>
+template <bool NT, class T>
 __device__ __forceinline__ void st_stream(T *p, T v) {
-#if NTTMUL_NT
-  __builtin_nontemporal_store(v, p);
-#else
-  *p = v;
-#endif
+  if constexpr (NT)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
 }
 
 // Forward CT stages of group g on NPOLY (1 or 2) polynomials (same twiddles).  SKIP: leave out
@@ -458,6 +460,7 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
   using W = typename A::word;
   using Gr = Groups<LOGS>;
   constexpr int N = Gr::N, TP = N / 16, PB = rows_threads(LOGS) / TP, G = Gr::G, NP = Gr::NP;
+  constexpr bool kNT = NTTMUL_NT && (L1 == 0 || NTTMUL_NT_MP);
   __shared__ W lds[PB][lds_regions<W>()][NP];
 
   const int pb = threadIdx.x / TP, j = threadIdx.x % TP;
@@ -479,8 +482,8 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
 #else
 #pragma unroll
   for (int k = 0; k < 16; k++) {
-    x[k] = to_word<W>(ld_stream(a + base_l + Gr::off(0, k)));
-    y[k] = to_word<W>(ld_stream(b + base_l + Gr::off(0, k)));
+    x[k] = to_word<W>(ld_stream<kNT>(a + base_l + Gr::off(0, k)));
+    y[k] = to_word<W>(ld_stream<kNT>(b + base_l + Gr::off(0, k)));
   }
 #endif
   W *lx = lds[pb][0], *ly = lds[pb][lds_regions<W>() - 1];
@@ -501,7 +504,7 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
     for (int k = 0; k < 16; k++) {
       W v = x[k];
       if (L1 == 0 && !A::kInvCanonical) v = P.ar.canon(v);
-      st_stream(c + base_g + Gr::off(0, k), (TOut)v);
+      st_stream<kNT>(c + base_g + Gr::off(0, k), (TOut)v);
     }
   }
 }
@@ -692,7 +695,10 @@ static KParams<A> make_params(const LaunchTables &T) {
   KParams<A> P;
   P.ar.q = (W)T.q;
   P.ar.qinv_neg = (W)T.qinv_neg;
-  if constexpr (IsPlantard<A>::value) P.ar.c32 = (uint32_t)((1ull << 32) % T.q);
+  if constexpr (IsPlantard<A>::value) {
+    P.ar.c32 = (uint32_t)((1ull << 32) % T.q);
+    P.ar.as = (uint32_t)((3 * T.q + 1) / 2);
+  }
   P.fw = (const TwPair<W> *)T.fw;
   P.iw = (const TwPair<W> *)T.iw;
   P.f = (W)T.f; P.fs = (W)T.fs; P.wf = (W)T.wf; P.wfs = (W)T.wfs;

@@ -324,6 +324,7 @@ struct Arith32P {
   uint32_t q;
   uint32_t qinv_neg;  // -q^-1 mod 2^32 (Montgomery reduction of the base-multiplication sums)
   uint32_t c32;       // 2^32 mod q
+  uint32_t as;        // ceil(1.5 q): the signed-input Plantard addend (pmul_s)
 
   __device__ __forceinline__ static uint32_t csub(uint32_t x, uint32_t m) {
     uint32_t d;
@@ -339,8 +340,25 @@ struct Arith32P {
     return (uint32_t)(((uint64_t)th * q + q) >> 32);
 #endif
   }
+  // x w mod q in [0, q) for int32 x in (-q, q) (also any int32 but -q, -2q...), with the
+  // signed pair (b0, b1 + (b0 >> 31)) of the planner: T = x BR mod 2^64 through v_mul_hi_i32, and
+  // t = floor((T_hi q + A) / 2^32) is exact for A in [q + 2^31 q / 2^32, 2^32 - 2^31 q / 2^32),
+  // non-empty for q < 2^31 (the error term spans 2^32 q < 2^32 (2^32 - q)); A = ceil(1.5 q)
+  __device__ __forceinline__ uint32_t pmul_s(uint32_t x, uint32_t b0, uint32_t b1s) const {
+    const uint32_t th = (uint32_t)__mulhi((int)x, (int)b0) + x * b1s;
+    return (uint32_t)(((uint64_t)th * q + as) >> 32);
+  }
   __device__ __forceinline__ uint32_t shoup(uint32_t x, uint32_t b0, uint32_t b1) const {
     return pmul(x, b0, b1);
+  }
+  // inverse-table product of a GS difference x - y (x, y canonical)
+  __device__ __forceinline__ uint32_t pmul_diff(uint32_t x, uint32_t y, uint32_t b0,
+                                                uint32_t b1) const {
+#if NTTMUL_P_SIGNED_INV
+    return pmul_s(x - y, b0, b1);
+#else
+    return pmul(x - y + q, b0, b1);
+#endif
   }
   // CT (ntt.C:365-367 pattern): X in [0, 2q) (XC: canonical; XN: signed in (-q, q)), Y any ->
   // X' in [0, 2q), Y' in (0, 2q) (YN: x - t signed in (-q, q), for a register whose next use is
@@ -364,14 +382,14 @@ struct Arith32P {
   __device__ __forceinline__ void gs(uint32_t &X, uint32_t &Y, uint32_t b0, uint32_t b1) const {
     const uint32_t x = X, y = Y;
     X = csub(x + y, q);
-    Y = pmul(x - y + q, b0, b1);
+    Y = pmul_diff(x, y, b0, b1);
   }
   // last inverse stage with the output scale F folded in: ((X + Y) F, (X - Y) w F), canonical
   __device__ __forceinline__ void gs_scaled(uint32_t &X, uint32_t &Y, uint32_t f0, uint32_t f1,
                                             uint32_t wf0, uint32_t wf1) const {
     const uint32_t x = X, y = Y;
     X = pmul(x + y, f0, f1);
-    Y = pmul(x - y + q, wf0, wf1);
+    Y = pmul_diff(x, y, wf0, wf1);
   }
   // Montgomery a b 2^-32 mod q, a and b in [0, 2q) -> [0, q): a reduced below q, so
   // a b + m q < 2 q^2 + 2^32 q < 2^64 and the quotient is below 2q

@@ -77,7 +77,9 @@ static uint64_t companion(uint64_t w, uint64_t q, int bits) {
 // Arith32P (arith_select.hpp) the Plantard constant BR = B q^-1 mod 2^64, B = -w 2^64 mod q, as
 // (low, high) words; for the other 32-bit classes the Montgomery form (w 2^32 mod q, that times
 // -q^-1 mod 2^32)
-static void tw_pair(uint64_t w, uint64_t q, int bits, uint64_t *v, uint64_t *c) {
+// sgn (Arith32P only): the pair for a signed multiplicand x in [-2^31, 2^31) — the high word
+// absorbs the sign of the low one (v_mul_hi_i32 reads it as int32): c + (v >> 31)
+static void tw_pair(uint64_t w, uint64_t q, int bits, uint64_t *v, uint64_t *c, bool sgn = false) {
   if (bits == 32 && a32_kind(q) == A32Kind::Plantard) {
     uint64_t inv = q;  // q^-1 mod 2^64 (Newton on the 2-adic inverse)
     for (int i = 0; i < 6; i++) inv *= 2 - q * inv;
@@ -86,6 +88,7 @@ static void tw_pair(uint64_t w, uint64_t q, int bits, uint64_t *v, uint64_t *c) 
     const uint64_t br = b * inv;
     *v = br & 0xFFFFFFFFull;
     *c = br >> 32;
+    if (sgn && NTTMUL_P_SIGNED_INV) *c = (*c + (*v >> 31)) & 0xFFFFFFFFull;
     return;
   }
   // Arith32W (q >= 2^31) always takes the Montgomery form
@@ -106,12 +109,12 @@ static void tw_pair(uint64_t w, uint64_t q, int bits, uint64_t *v, uint64_t *c) 
 
 template <class W>
 static void put_pairs(std::vector<uint8_t> &dst, const std::vector<uint64_t> &w, uint64_t q,
-                      int bits) {
+                      int bits, bool sgn = false) {
   dst.assign(w.size() * 2 * sizeof(W), 0);
   W *p = (W *)dst.data();
   for (size_t i = 0; i < w.size(); i++) {
     uint64_t v, c;
-    tw_pair(w[i], q, bits, &v, &c);
+    tw_pair(w[i], q, bits, &v, &c, sgn);
     p[2 * i] = (W)v;
     p[2 * i + 1] = (W)c;
   }
@@ -212,7 +215,7 @@ int make_plan(uint32_t n, uint64_t q, uint64_t psi, Plan *P, bool cyclic) {
   }
   if (bits == 32) {
     put_pairs<uint32_t>(P->fw, fw, q, 32);
-    put_pairs<uint32_t>(P->iw, iw, q, 32);
+    put_pairs<uint32_t>(P->iw, iw, q, 32, true);  // GS multiplicands are differences
     if (NTTMUL_A32_MONT && a32_kind(q) == A32Kind::Mont) {  // typed butterflies: centred copies
       append_centred(P->fw, n, q);
       append_centred(P->iw, n, q);
@@ -230,16 +233,16 @@ int make_plan(uint32_t n, uint64_t q, uint64_t psi, Plan *P, bool cyclic) {
   const uint64_t r_mod_q = (uint64_t)(((u128)1 << bits) % q);
   const uint64_t f = mulmod(P->inv_n, r_mod_q, q);
   tw_pair(f, q, bits, &P->f, &P->fs);
-  tw_pair(mulmod(iw[1], f, q), q, bits, &P->wf, &P->wfs);
+  tw_pair(mulmod(iw[1], f, q), q, bits, &P->wf, &P->wfs, true);
   const uint64_t f4 = mulmod(f, 4, q);
   tw_pair(f4, q, bits, &P->f4, &P->f4s);
-  tw_pair(mulmod(iw[1], f4, q), q, bits, &P->wf4, &P->wf4s);
+  tw_pair(mulmod(iw[1], f4, q), q, bits, &P->wf4, &P->wf4s, true);
   // standalone inverse NTT: plain n^-1 (ntt256.C:12); pointwise product: R^2 mod q
   tw_pair(P->inv_n, q, bits, &P->fi, &P->fis);
-  tw_pair(mulmod(iw[1], P->inv_n, q), q, bits, &P->wfi, &P->wfis);
+  tw_pair(mulmod(iw[1], P->inv_n, q), q, bits, &P->wfi, &P->wfis, true);
   // the reference's unscaled inverses (intt*, inttmul*: intt(ntt(a)) = n a, ntt256.h:16-17)
   tw_pair(1, q, bits, &P->fu, &P->fus);
-  tw_pair(iw[1], q, bits, &P->wfu, &P->wfus);
+  tw_pair(iw[1], q, bits, &P->wfu, &P->wfus, true);
   P->r2 = mulmod(r_mod_q, r_mod_q, q);
   return NTTMUL_OK;
 }

@@ -4,7 +4,7 @@ set -o pipefail
 OUT=gpurun_out/${1:-c5sweep}
 mkdir -p $OUT
 for lanes in 1 2; do
-  for mb in 16 32 64 128 256; do
+  for mb in ${MBS:-16 32 64 128 256 512}; do
     NTTMUL_MP_LANES=$lanes NTTMUL_MP_CHUNK_MB=$mb timeout -k 10 120 python bench.py --n 65536 \
       --q 4611686018425815041 --batch-per-gpu 1024 --steps 30 --warmup 10 --no-cpu-baseline \
       > $OUT/l${lanes}_mb$mb.json 2>/dev/null || exit 1

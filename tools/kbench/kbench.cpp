@@ -43,9 +43,33 @@ int main(int argc, char **argv) {
   for (int i = 0; i < 3; i++) CK(nttmul::launch_polymul(T, a, b, c, batch, io_bits, scr, 0));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  CK(hipEventRecord(e0, 0));
-  for (int i = 0; i < reps; i++) CK(nttmul::launch_polymul(T, a, b, c, batch, io_bits, scr, 0));
-  CK(hipEventRecord(e1, 0));
+  // KB_STREAMS=2: consecutive launches alternate over two streams with their own c buffer (a and
+  // b are read-only), so one launch's tail overlaps the next one's ramp
+  const int nstreams = getenv("KB_STREAMS") ? atoi(getenv("KB_STREAMS")) : 1;
+  hipStream_t st[2] = {0, 0};
+  void *c2 = c;
+  hipEvent_t join;
+  CK(hipEventCreateWithFlags(&join, hipEventDisableTiming));
+  if (nstreams == 2) {
+    CK(hipStreamCreateWithFlags(&st[0], hipStreamNonBlocking));
+    CK(hipStreamCreateWithFlags(&st[1], hipStreamNonBlocking));
+    CK(hipMalloc(&c2, bytes));
+    CK(hipDeviceSynchronize());
+  }
+  CK(hipEventRecord(e0, st[0]));
+  if (nstreams == 2) {
+    CK(hipEventRecord(join, st[0]));
+    CK(hipStreamWaitEvent(st[1], join, 0));
+  }
+  for (int i = 0; i < reps; i++) {
+    const int k = nstreams == 2 ? (i & 1) : 0;
+    CK(nttmul::launch_polymul(T, a, b, k ? c2 : c, batch, io_bits, scr, st[k]));
+  }
+  if (nstreams == 2) {
+    CK(hipEventRecord(join, st[1]));
+    CK(hipStreamWaitEvent(st[0], join, 0));
+  }
+  CK(hipEventRecord(e1, st[0]));
   CK(hipEventSynchronize(e1));
   float ms;
   CK(hipEventElapsedTime(&ms, e0, e1));
