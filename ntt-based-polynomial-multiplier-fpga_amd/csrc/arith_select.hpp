@@ -20,7 +20,45 @@
 #define NTTMUL_P_SIGNED_INV 1
 #endif
 
+// column stages of the n = 65536 multi-pass product (4: 16 x 4096 rows, 5: 32 x 2048)
+#ifndef NTTMUL_SPLIT16
+#define NTTMUL_SPLIT16 4
+#endif
+// Arith32P forward CT typing: 0 = off; 1 = a difference x - t stays signed when its next use in
+// the register group is as an X; 2 = every in-group difference stays signed and is multiplied by
+// the signed-input Plantard product, so the planner stores those forward twiddles in signed form
+// (p_signed_fw_entry); planner and kernels must agree
+#ifndef NTTMUL_P_TYPED
+#define NTTMUL_P_TYPED 2
+#endif
+
 namespace nttmul {
+
+// log2 of the rows a product / transform runs in registers + LDS (kernels.hip k_rows, k_xform):
+// the whole polynomial up to n = 4096, else 4096-coefficient rows after L1 = logn - LOGS column
+// stages
+constexpr int row_logs(int logn) {
+  return logn <= 12 ? logn : (logn == 16 && NTTMUL_SPLIT16 == 5 ? 11 : 12);
+}
+// register groups of a row of 2^LOGS coefficients (kernels.hip Groups<LOGS>::G / S / ST0)
+constexpr int groups_g(int logs) { return (logs + 3) / 4; }
+constexpr int groups_s(int logs, int g) {
+  return logs / groups_g(logs) + (g < logs % groups_g(logs) ? 1 : 0);
+}
+// Arith32P, NTTMUL_P_TYPED == 2: forward twiddle entry idx = 2^st + j serves stage st; at a
+// stage that is not the first of its register group, the multiplicand of the butterflies using
+// an odd entry is the previous stage's difference (bit 2d of the element = the entry's low bit),
+// kept signed: that entry is stored in the signed-input form
+constexpr bool p_signed_fw_entry(int logn, uint32_t idx) {
+  if (idx < 2) return false;
+  int st = 0;
+  while ((2u << st) <= idx) st++;
+  const int logs = row_logs(logn), local = st - (logn - logs);
+  if (local < 0) return false;  // column pass: unsigned operands
+  int g = 0, st0 = 0;
+  while (st0 + groups_s(logs, g) <= local) st0 += groups_s(logs, g++);
+  return local - st0 >= 1 && (idx & 1);
+}
 
 enum class A32Kind { Harvey, Plantard, Mont, Wide };
 

@@ -63,10 +63,7 @@
 #ifndef NTTMUL_PAD0
 #define NTTMUL_PAD0 1
 #endif
-// column stages of the n = 65536 multi-pass product (4: 16 x 4096 rows, 5: 32 x 2048)
-#ifndef NTTMUL_SPLIT16
-#define NTTMUL_SPLIT16 4
-#endif
+// NTTMUL_SPLIT16 (column stages of the n = 65536 multi-pass product): arith_select.hpp
 #ifndef NTTMUL_ABL_NOLOAD
 #define NTTMUL_ABL_NOLOAD 0
 #endif
@@ -153,6 +150,16 @@ struct Groups {
   static constexpr int NP = N + N / 16;  // padded LDS words per polynomial (>= every padx)
 };
 
+template <int LOGS>
+constexpr bool groups_agree() {
+  for (int g = 0; g < Groups<LOGS>::G; g++)
+    if (Groups<LOGS>::S(g) != groups_s(LOGS, g)) return false;
+  return Groups<LOGS>::G == groups_g(LOGS);
+}
+static_assert(groups_agree<8>() && groups_agree<9>() && groups_agree<10>() && groups_agree<11>() &&
+                  groups_agree<12>(),
+              "arith_select.hpp's group helpers (planner twiddle forms) must match Groups<>");
+
 template <class W, class T>
 __device__ __forceinline__ W to_word(T v) { return (W)v; }
 
@@ -238,7 +245,8 @@ __device__ __forceinline__ void fwd_group(const A &ar, typename A::word (&x)[16]
         // bit 2 dist is set; this stage leaves its difference in k + dist signed iff the next
         // stage of the group uses that register as an X (bit dist / 2 clear)
         const bool xn = l > 0 && (k & (2 * dist));
-        const bool yn = l < S - SKIP - 1 && !((k + dist) & (dist >> 1));
+        const bool yn = NTTMUL_P_TYPED >= 2 ? l < S - SKIP - 1
+                                            : l < S - SKIP - 1 && !((k + dist) & (dist >> 1));
         const bool xc = NTTMUL_FIRST_XC && g == 0 && l == 0 && l1 == 0;
 #define NTTMUL_CT_P(XC_, XN_, YN_)                                         \
   do {                                                                     \
@@ -419,7 +427,9 @@ __device__ __forceinline__ void base_mult(const A &ar, typename A::word (&x)[16]
       // typed arithmetic: the last forward stage (dist 8 >> (S - D - 1)) multiplied N-type
       // operands, and so kept the centred twiddle, when bit 2 dist of its X register is set
       constexpr int dl = 8 >> (Gr::S(g) - D - 1);
-      const bool zc = A::kTyped && Gr::S(g) - D - 1 > 0 && (kz & (2 * dl));
+      // (Arith32P, NTTMUL_P_TYPED 2: the same condition says the pair is in signed form)
+      constexpr bool typed_z = A::kTyped || (kTypedP<A>() && NTTMUL_P_TYPED >= 2);
+      const bool zc = typed_z && Gr::S(g) - D - 1 > 0 && (kz & (2 * dl));
       typename A::word a[B], b[B];
 #pragma unroll
       for (int i = 0; i < B; i++) a[i] = x[r[i]], b[i] = y[r[i]];

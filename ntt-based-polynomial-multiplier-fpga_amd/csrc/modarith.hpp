@@ -306,9 +306,7 @@ using Arith32H = Arith32T<true>;   // q < 2^30
 //   CT  (forward, x lazy in [0, 2q), Y any word): x = csub(X); t = x w; (x + t, x - t + q)
 //   GS  (inverse, x, y canonical): (csub(x + y), (x - y + q) w), both outputs canonical
 // Every inverse value is canonical, so the transform's output needs no final canonicalisation.
-#ifndef NTTMUL_P_TYPED  // Arith32P: CT differences that feed an addition stay signed (no "+ q")
-#define NTTMUL_P_TYPED 1
-#endif
+// NTTMUL_P_TYPED (Arith32P CT differences kept signed): arith_select.hpp
 #ifndef NTTMUL_P_HI  // Arith32P: last Plantard step as v_mul_hi_u32(th + 1, q) (A/B variant)
 #define NTTMUL_P_HI 0
 #endif
@@ -374,7 +372,8 @@ struct Arith32P {
     } else {
       x = csub(X, q);
     }
-    const uint32_t t = pmul(Y, b0, b1);
+    // NTTMUL_P_TYPED 2: an N-type X comes with an N-type Y and a signed-form twiddle pair
+    const uint32_t t = XN && NTTMUL_P_TYPED >= 2 ? pmul_s(Y, b0, b1) : pmul(Y, b0, b1);
     X = x + t;
     Y = YN ? x - t : x - t + q;
   }
@@ -419,7 +418,8 @@ struct Arith32P {
     }
 #pragma unroll
     for (int i = 1; i < B; i++) {
-      const uint32_t t = pmul(b[i], w0, w1);
+      // ZC: the z pair is in signed form (NTTMUL_P_TYPED 2): multiply the canonical b_i
+      const uint32_t t = ZC ? pmul_s(br[i], w0, w1) : pmul(b[i], w0, w1);
       bz[i] = NEG ? q - t : t;
     }
 #pragma unroll

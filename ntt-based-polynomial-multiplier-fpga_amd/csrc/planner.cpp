@@ -88,7 +88,7 @@ static void tw_pair(uint64_t w, uint64_t q, int bits, uint64_t *v, uint64_t *c, 
     const uint64_t br = b * inv;
     *v = br & 0xFFFFFFFFull;
     *c = br >> 32;
-    if (sgn && NTTMUL_P_SIGNED_INV) *c = (*c + (*v >> 31)) & 0xFFFFFFFFull;
+    if (sgn) *c = (*c + (*v >> 31)) & 0xFFFFFFFFull;
     return;
   }
   // Arith32W (q >= 2^31) always takes the Montgomery form
@@ -107,14 +107,18 @@ static void tw_pair(uint64_t w, uint64_t q, int bits, uint64_t *v, uint64_t *c, 
   *c = companion(w, q, bits);
 }
 
+// fw_logn > 0: forward table of an Arith32P plan with NTTMUL_P_TYPED 2: the entries whose
+// multiplicand is a signed in-group difference get the signed form (arith_select.hpp)
 template <class W>
 static void put_pairs(std::vector<uint8_t> &dst, const std::vector<uint64_t> &w, uint64_t q,
-                      int bits, bool sgn = false) {
+                      int bits, bool sgn = false, int fw_logn = 0) {
   dst.assign(w.size() * 2 * sizeof(W), 0);
   W *p = (W *)dst.data();
   for (size_t i = 0; i < w.size(); i++) {
     uint64_t v, c;
-    tw_pair(w[i], q, bits, &v, &c, sgn);
+    const bool s = sgn || (fw_logn > 0 && NTTMUL_P_TYPED >= 2 && a32_kind(q) == A32Kind::Plantard &&
+                           p_signed_fw_entry(fw_logn, (uint32_t)i));
+    tw_pair(w[i], q, bits, &v, &c, s);
     p[2 * i] = (W)v;
     p[2 * i + 1] = (W)c;
   }
@@ -214,8 +218,8 @@ int make_plan(uint32_t n, uint64_t q, uint64_t psi, Plan *P, bool cyclic) {
     }
   }
   if (bits == 32) {
-    put_pairs<uint32_t>(P->fw, fw, q, 32);
-    put_pairs<uint32_t>(P->iw, iw, q, 32, true);  // GS multiplicands are differences
+    put_pairs<uint32_t>(P->fw, fw, q, 32, false, (int)P->logn);
+    put_pairs<uint32_t>(P->iw, iw, q, 32, NTTMUL_P_SIGNED_INV);  // GS multiplicands: differences
     if (NTTMUL_A32_MONT && a32_kind(q) == A32Kind::Mont) {  // typed butterflies: centred copies
       append_centred(P->fw, n, q);
       append_centred(P->iw, n, q);
@@ -233,16 +237,16 @@ int make_plan(uint32_t n, uint64_t q, uint64_t psi, Plan *P, bool cyclic) {
   const uint64_t r_mod_q = (uint64_t)(((u128)1 << bits) % q);
   const uint64_t f = mulmod(P->inv_n, r_mod_q, q);
   tw_pair(f, q, bits, &P->f, &P->fs);
-  tw_pair(mulmod(iw[1], f, q), q, bits, &P->wf, &P->wfs, true);
+  tw_pair(mulmod(iw[1], f, q), q, bits, &P->wf, &P->wfs, NTTMUL_P_SIGNED_INV);
   const uint64_t f4 = mulmod(f, 4, q);
   tw_pair(f4, q, bits, &P->f4, &P->f4s);
-  tw_pair(mulmod(iw[1], f4, q), q, bits, &P->wf4, &P->wf4s, true);
+  tw_pair(mulmod(iw[1], f4, q), q, bits, &P->wf4, &P->wf4s, NTTMUL_P_SIGNED_INV);
   // standalone inverse NTT: plain n^-1 (ntt256.C:12); pointwise product: R^2 mod q
   tw_pair(P->inv_n, q, bits, &P->fi, &P->fis);
-  tw_pair(mulmod(iw[1], P->inv_n, q), q, bits, &P->wfi, &P->wfis, true);
+  tw_pair(mulmod(iw[1], P->inv_n, q), q, bits, &P->wfi, &P->wfis, NTTMUL_P_SIGNED_INV);
   // the reference's unscaled inverses (intt*, inttmul*: intt(ntt(a)) = n a, ntt256.h:16-17)
   tw_pair(1, q, bits, &P->fu, &P->fus);
-  tw_pair(iw[1], q, bits, &P->wfu, &P->wfus, true);
+  tw_pair(iw[1], q, bits, &P->wfu, &P->wfus, NTTMUL_P_SIGNED_INV);
   P->r2 = mulmod(r_mod_q, r_mod_q, q);
   return NTTMUL_OK;
 }
