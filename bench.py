@@ -81,6 +81,10 @@ def parse(argv=None):
                     help="cycle the steps over this many distinct (a, b, c) buffer sets, so a "
                          "batch smaller than the Infinity Cache is still read from HBM "
                          "(0: auto = enough sets for 3 x 256 MiB when the batch fits in it, else 1)")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="alternate consecutive steps over this many HIP streams (default 1; 2 "
+                         "overlaps one launch's tail with the next one's ramp: a C2-sized batch "
+                         "is a single generation of workgroups)")
     ap.add_argument("--dump-samples", default="",
                     help="write <prefix>.rank<r>.npz with sampled products of this rank's slice "
                          "(checked against the oracle by tests/test_gpu_parity.py)")
@@ -262,11 +266,17 @@ def main(argv=None):
     wbytes = wb // 8
     alg_bytes = 3 * n * wbytes * count                    # read a, b + write c, per launch
     rotate = buffer_sets(alg_bytes, args.rotate)
+    nstreams = max(1, args.streams)
+    if nstreams > 1:  # concurrent steps never share an output buffer
+        rotate = max(rotate, nstreams)
 
     ctx = nttmul.Context(n, q, ndev=1, first_dev=devno)
     dt = torch.int32 if wb == 32 else torch.int64
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
+    # --streams S: consecutive steps alternate over S streams, so one launch's store tail and the
+    # next one's load ramp overlap (a batch that is a single generation of workgroups, C2)
+    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(nstreams - 1)]
     sets = []
     for _ in range(rotate):   # identical inputs in every set (same counter range)
         a = torch.empty(count * n, dtype=dt, device=dev)
@@ -277,8 +287,9 @@ def main(argv=None):
 
     def step():
         a, b, c = sets[state["i"] % rotate]
+        st = streams[state["i"] % nstreams]
         state["i"] += 1
-        ctx.multiply_device(c, a, b, count, wb, stream=sptr)
+        ctx.multiply_device(c, a, b, count, wb, stream=st.cuda_stream)
 
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
@@ -287,9 +298,13 @@ def main(argv=None):
     def timed_step():  # HIP events on the launch stream around the K timed steps
         if events["n"] == args.warmup:
             ev0.record(stream)
+            for st in streams[1:]:  # the other streams' timed steps start after ev0
+                st.wait_event(ev0)
         step()
         events["n"] += 1
         if events["n"] == args.warmup + args.steps:
+            for st in streams[1:]:  # ev1 after every stream's last timed step
+                stream.wait_event(st.record_event())
             ev1.record(stream)
 
     wall = timed_steps(timed_step, args.steps, args.warmup, lambda: torch.cuda.synchronize(dev),
@@ -341,10 +356,16 @@ def main(argv=None):
                          "kernel_ms": kern_ms,
                          "alg_bytes_per_launch": alg_bytes,
                          "buffer_sets": rotate,
+                         "streams": nstreams,
                          "cache_resident": resident},
             "build": {"code_object": co},
             "cpu_baseline": None,
         }
+        if nstreams > 1:
+            line["roofline"]["streams_note"] = (
+                f"consecutive steps alternate over {nstreams} HIP streams; kernel_ms is the time "
+                "per step over the K timed steps (launches overlap, so a single dispatch in a "
+                "profiler trace lasts longer)")
         if rotate > 1:
             line["roofline"]["note"] = (
                 f"one step's a, b, c ({alg_bytes / 2**20:.0f} MiB) fit the 256 MiB Infinity "
