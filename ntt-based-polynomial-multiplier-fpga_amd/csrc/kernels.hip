@@ -245,8 +245,11 @@ __device__ __forceinline__ void fwd_group(const A &ar, typename A::word (&x)[16]
         // bit 2 dist is set; this stage leaves its difference in k + dist signed iff the next
         // stage of the group uses that register as an X (bit dist / 2 clear)
         const bool xn = l > 0 && (k & (2 * dist));
-        const bool yn = NTTMUL_P_TYPED >= 2 ? l < S - SKIP - 1
-                                            : l < S - SKIP - 1 && !((k + dist) & (dist >> 1));
+        // (P_TYPED 2: the last stage before the base multiplication leaves its differences
+        // signed as well; Arith32P::basemul corrects the -w blocks with the carry of x + q)
+        const bool yn = NTTMUL_P_TYPED >= 2
+                            ? l < S - SKIP - 1 || (SKIP > 0 && g + 1 == Gr::G)
+                            : l < S - SKIP - 1 && !((k + dist) & (dist >> 1));
         const bool xc = NTTMUL_FIRST_XC && g == 0 && l == 0 && l1 == 0;
 #define NTTMUL_CT_P(XC_, XN_, YN_)                                         \
   do {                                                                     \

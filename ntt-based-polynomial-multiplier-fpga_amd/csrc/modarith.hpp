@@ -328,6 +328,11 @@ struct Arith32P {
     uint32_t d;
     return __builtin_sub_overflow(x, m, &d) ? x : d;
   }
+  // int32 x in (-q, q) -> [0, q): the carry of x + q is set exactly when x < 0
+  __device__ __forceinline__ uint32_t cadd(uint32_t x) const {
+    uint32_t e;
+    return __builtin_add_overflow(x, q, &e) ? e : x;
+  }
   // x w mod q in [0, q) for any 32-bit x; (b0, b1) = the planner's Plantard pair of w
   __device__ __forceinline__ uint32_t pmul(uint32_t x, uint32_t b0, uint32_t b1) const {
     const uint32_t th = __umulhi(x, b0) + x * b1;
@@ -410,16 +415,19 @@ struct Arith32P {
   __device__ __forceinline__ void basemul(uint32_t (&a)[B], const uint32_t (&b)[B], uint32_t w0,
                                           uint32_t w1) const {
     static_assert(B == 4, "sums of B products must fit 64 bits");
+    // a -w block (x^4 + w) holds the last forward stage's differences: with NTTMUL_P_TYPED 2 they
+    // arrive signed in (-q, q) and are corrected by the carry of x + q
+    constexpr bool kN = NEG && NTTMUL_P_TYPED >= 2;
     uint32_t ar[B], br[B], bz[B];
 #pragma unroll
     for (int i = 0; i < B; i++) {
-      ar[i] = csub(a[i], q);
-      br[i] = csub(b[i], q);
+      ar[i] = kN ? cadd(a[i]) : csub(a[i], q);
+      br[i] = kN ? cadd(b[i]) : csub(b[i], q);
     }
 #pragma unroll
     for (int i = 1; i < B; i++) {
       // ZC: the z pair is in signed form (NTTMUL_P_TYPED 2): multiply the canonical b_i
-      const uint32_t t = ZC ? pmul_s(br[i], w0, w1) : pmul(b[i], w0, w1);
+      const uint32_t t = ZC ? pmul_s(br[i], w0, w1) : pmul(kN ? br[i] : b[i], w0, w1);
       bz[i] = NEG ? q - t : t;
     }
 #pragma unroll
