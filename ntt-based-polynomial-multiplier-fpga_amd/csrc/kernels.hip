@@ -484,6 +484,11 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
   // threads past the batch end read unit 0 (always valid) instead of branching per load; their
   // results are never stored
   const size_t base_l = live ? base_g : (size_t)Gr::base(0, j);
+#ifdef NTTMUL_ABL_L2LOAD  // ablation: every unit reads one of the first 64 units (L2-resident)
+  const size_t base_r = (u & 63) * N + Gr::base(0, j);
+#else
+  const size_t base_r = base_l;
+#endif
 
   W x[16], y[16];
 #if NTTMUL_ABL_NOLOAD
@@ -495,8 +500,8 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
 #else
 #pragma unroll
   for (int k = 0; k < 16; k++) {
-    x[k] = to_word<W>(ld_stream<kNT>(a + base_l + Gr::off(0, k)));
-    y[k] = to_word<W>(ld_stream<kNT>(b + base_l + Gr::off(0, k)));
+    x[k] = to_word<W>(ld_stream<kNT>(a + base_r + Gr::off(0, k)));
+    y[k] = to_word<W>(ld_stream<kNT>(b + base_r + Gr::off(0, k)));
   }
 #endif
   W *lx = lds[pb][0], *ly = lds[pb][lds_regions<W>() - 1];
