@@ -30,6 +30,10 @@ for cfg in $CFGS; do
     c3) one c3 ;;
     c5) one c5 --n 65536 --q 4611686018425815041 --batch-per-gpu 1024 --steps 30 --warmup 10 ;;
     c2) one c2 --n 1024 --batch-per-gpu 4096 --steps 300 --warmup 50 ;;
+    c2s) mkdir -p gpurun_out/$TAG/c2s  # two streams: bench line only (same kernel as c2)
+         run 300 python bench.py --n 1024 --batch-per-gpu 4096 --steps 300 --warmup 50 --streams 2 \
+           --no-cpu-baseline > gpurun_out/$TAG/c2s/bench.json 2> gpurun_out/$TAG/c2s/bench.err
+         tail -c 400 gpurun_out/$TAG/c2s/bench.json >&2 ;;
   esac
 done
 echo "done $TAG" >&2
