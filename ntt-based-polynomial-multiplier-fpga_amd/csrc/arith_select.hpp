@@ -60,6 +60,20 @@ constexpr bool p_signed_fw_entry(int logn, uint32_t idx) {
   return local - st0 >= 1 && (idx & 1);
 }
 
+// Arith32P3 (base blocks of 8 coefficients, n = 4096 products only): each output sums eight
+// products of canonical values; the first four are folded by 2^32 mod q before the other four
+// are added, which keeps the sum below 2^64 only when 2^32 mod q is small enough
+#ifndef NTTMUL_P3
+#define NTTMUL_P3 1
+#endif
+constexpr bool p3_fold_ok(uint64_t q) {
+  if (!NTTMUL_P3 || q >= (1ull << 31) || q < (1ull << 30)) return false;
+  const unsigned __int128 s1 = (unsigned __int128)4 * (q - 1) * (q - 1);  // < 2^64
+  const unsigned __int128 c32 = ((unsigned __int128)1 << 32) % q;
+  const unsigned __int128 fold = (s1 >> 32) * c32 + 0xFFFFFFFFu;
+  return fold + s1 < ((unsigned __int128)1 << 64);
+}
+
 enum class A32Kind { Harvey, Plantard, Mont, Wide };
 
 // q < 2^32 only (64-bit words take Arith64)

@@ -168,6 +168,8 @@ template <class A>
 struct IsPlantard : std::false_type {};
 template <>
 struct IsPlantard<Arith32P> : std::true_type {};
+template <>
+struct IsPlantard<Arith32P3> : std::true_type {};
 template <class A>
 __host__ __device__ constexpr bool kTypedP() {
   if constexpr (IsPlantard<A>::value) return A::kTypedP;
@@ -729,9 +731,12 @@ template <class A>
 static KParams<A> product_params(const LaunchTables &T) {
   using W = typename A::word;
   KParams<A> P = make_params<A>(T);
-  static_assert(A::kBaseD == 0 || A::kBaseD == 2, "planner provides F 2^D for D = 2 only");
+  static_assert(A::kBaseD == 0 || A::kBaseD == 2 || A::kBaseD == 3,
+                "planner provides F 2^D for D = 2, 3");
   if (NTTMUL_BASE_D && A::kBaseD == 2) {
     P.f = (W)T.f4; P.fs = (W)T.f4s; P.wf = (W)T.wf4; P.wfs = (W)T.wf4s;
+  } else if (NTTMUL_BASE_D && A::kBaseD == 3) {
+    P.f = (W)T.f8; P.fs = (W)T.f8s; P.wf = (W)T.wf8; P.wfs = (W)T.wf8s;
   }
   return P;
 }
@@ -800,6 +805,13 @@ template <class A>
 static hipError_t polymul_io(const LaunchTables &T, const void *a, const void *b, void *c,
                              size_t batch, int io_bits, void **scr, hipStream_t s) {
   const bool big = T.logn > 12;
+  if constexpr (std::is_same<A, Arith32P>::value) {  // D = 3 blocks at n = 4096 (Arith32P3)
+    if (T.logn == 12 && p3_fold_ok(T.q)) {
+      const KParams<Arith32P3> P = product_params<Arith32P3>(T);
+      return io_bits == 64 ? launch_rows<Arith32P3, uint64_t, uint64_t, 12, 0>(P, a, b, c, batch, s)
+                           : launch_rows<Arith32P3, uint32_t, uint32_t, 12, 0>(P, a, b, c, batch, s);
+    }
+  }
   if (io_bits == 64)
     return big ? multipass<A, uint64_t>(T, a, b, c, batch, scr, s)
                : fused<A, uint64_t>(T, a, b, c, batch, s);
@@ -813,7 +825,11 @@ hipError_t launch_polymul(const LaunchTables &T, const void *a, const void *b, v
   if (T.word_bits != 32 || T.q >= (1ull << 31) || big || io_bits != 32) return hipErrorNotSupported;
   switch (a32_kind(T.q)) {
     case A32Kind::Harvey: return fused<Arith32H, uint32_t>(T, a, b, c, batch, s);
-    case A32Kind::Plantard: return fused<Arith32P, uint32_t>(T, a, b, c, batch, s);
+    case A32Kind::Plantard:
+      if (T.logn == 12 && p3_fold_ok(T.q))
+        return launch_rows<Arith32P3, uint32_t, uint32_t, 12, 0>(product_params<Arith32P3>(T), a,
+                                                                 b, c, batch, s);
+      return fused<Arith32P, uint32_t>(T, a, b, c, batch, s);
     default: return fused<Arith32, uint32_t>(T, a, b, c, batch, s);
   }
 #else

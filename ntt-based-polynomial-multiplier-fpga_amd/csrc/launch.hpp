@@ -13,6 +13,7 @@ struct LaunchTables {
   uint64_t q, qinv_neg;    // -q^-1 mod 2^word_bits
   uint64_t f, fs, wf, wfs; // F = n^-1 R mod q and iw[1] F, as (value, companion) pairs
   uint64_t f4, f4s, wf4, wf4s; // 4 F and iw[1] 4 F: products with incomplete transforms (D = 2)
+  uint64_t f8, f8s, wf8, wf8s; // 8 F and iw[1] 8 F (D = 3: Arith32P3)
   uint64_t fi, fis, wfi, wfis; // n^-1 and iw[1] n^-1 (standalone inverse), with companions
   uint64_t r2;             // R^2 mod q (standalone pointwise product)
   const void *fw, *iw;     // forward / inverse twiddle (value, companion) pairs, n entries

@@ -455,6 +455,48 @@ struct Arith32P {
   }
 };
 
+// Arith32P with base blocks of 8 coefficients (D = 3): one butterfly stage fewer in each of the
+// three transforms for a base multiplication of 8 x 8 products per block.  Each output's eight
+// products of canonical values are summed in two halves: the first four (< 4 q^2) are folded by
+// 2^32 mod q before the other four are added, so the sum stays below 2^64 only when 2^32 mod q
+// is small (arith_select.hpp p3_fold_ok: q = 15 2^27 + 1 has 2^32 mod q = 2^28 - 2); the launcher
+// takes this class only for such q, and only at n = 4096 (the last register group must hold more
+// than 3 stages).
+struct Arith32P3 : Arith32P {
+  static constexpr int kBaseD = 3;
+  template <int B, bool NEG, bool ZC = false>
+  __device__ __forceinline__ void basemul(uint32_t (&a)[B], const uint32_t (&b)[B], uint32_t w0,
+                                          uint32_t w1) const {
+    static_assert(B == 8, "D = 3 blocks");
+    constexpr bool kN = NEG && NTTMUL_P_TYPED >= 2;
+    uint32_t ar[B], br[B], bz[B];
+#pragma unroll
+    for (int i = 0; i < B; i++) {
+      ar[i] = kN ? cadd(a[i]) : csub(a[i], q);
+      br[i] = kN ? cadd(b[i]) : csub(b[i], q);
+    }
+#pragma unroll
+    for (int i = 1; i < B; i++) {
+      const uint32_t t = ZC ? pmul_s(br[i], w0, w1) : pmul(kN ? br[i] : b[i], w0, w1);
+      bz[i] = NEG ? q - t : t;
+    }
+#pragma unroll
+    for (int k = 0; k < B; k++) {
+      uint64_t s = 0;
+#pragma unroll
+      for (int i = 0; i < B / 2; i++)
+        s += (uint64_t)ar[i] * (i <= k ? br[k - i] : bz[B + k - i]);
+      s = (uint64_t)(uint32_t)(s >> 32) * c32 + (uint32_t)s;
+#pragma unroll
+      for (int i = B / 2; i < B; i++)
+        s += (uint64_t)ar[i] * (i <= k ? br[k - i] : bz[B + k - i]);
+      const uint64_t s2 = (uint64_t)(uint32_t)(s >> 32) * c32 + (uint32_t)s;
+      const uint32_t m = (uint32_t)s2 * qinv_neg;
+      a[k] = csub((uint32_t)((s2 + (uint64_t)m * q) >> 32), q);
+    }
+  }
+};
+
 // 2^31 <= q < 2^32 in 32-bit words: no room above q, so values stay canonical in [0, q) and every
 // sum / difference / product is reduced completely; the 65th bit of a Montgomery sum is the
 // carry of a 64-bit add.  About 14 VALU instructions per butterfly, against ~30 for taking this q

@@ -118,6 +118,7 @@ LaunchTables tables_for(const nttmul_ctx *ctx, const DevState &d) {
   T.qinv_neg = P.qinv_neg;
   T.f = P.f; T.fs = P.fs; T.wf = P.wf; T.wfs = P.wfs;
   T.f4 = P.f4; T.f4s = P.f4s; T.wf4 = P.wf4; T.wf4s = P.wf4s;
+  T.f8 = P.f8; T.f8s = P.f8s; T.wf8 = P.wf8; T.wf8s = P.wf8s;
   T.fi = P.fi; T.fis = P.fis; T.wfi = P.wfi; T.wfis = P.wfis; T.r2 = P.r2;
   T.fw = d.fw;
   T.iw = d.iw;

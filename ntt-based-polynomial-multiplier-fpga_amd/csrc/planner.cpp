@@ -241,6 +241,9 @@ int make_plan(uint32_t n, uint64_t q, uint64_t psi, Plan *P, bool cyclic) {
   const uint64_t f4 = mulmod(f, 4, q);
   tw_pair(f4, q, bits, &P->f4, &P->f4s);
   tw_pair(mulmod(iw[1], f4, q), q, bits, &P->wf4, &P->wf4s, NTTMUL_P_SIGNED_INV);
+  const uint64_t f8 = mulmod(f, 8, q);
+  tw_pair(f8, q, bits, &P->f8, &P->f8s);
+  tw_pair(mulmod(iw[1], f8, q), q, bits, &P->wf8, &P->wf8s, NTTMUL_P_SIGNED_INV);
   // standalone inverse NTT: plain n^-1 (ntt256.C:12); pointwise product: R^2 mod q
   tw_pair(P->inv_n, q, bits, &P->fi, &P->fis);
   tw_pair(mulmod(iw[1], P->inv_n, q), q, bits, &P->wfi, &P->wfis, NTTMUL_P_SIGNED_INV);

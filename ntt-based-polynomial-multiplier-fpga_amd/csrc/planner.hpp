@@ -42,6 +42,7 @@ struct Plan {
   // product with incomplete transforms (kernels.hip base_mult, D = 2): the inverse skips D
   // stages, so it leaves (n / 2^D) c and the scale is F 2^D
   uint64_t f4 = 0, f4s = 0, wf4 = 0, wf4s = 0;
+  uint64_t f8 = 0, f8s = 0, wf8 = 0, wf8s = 0;  // D = 3 (Arith32P3)
   // interleaved {w, w'} pairs (u32 or u64 each), n entries; entry 0 unused
   std::vector<uint8_t> fw, iw;
 };

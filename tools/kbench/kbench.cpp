@@ -37,6 +37,7 @@ int main(int argc, char **argv) {
   T.logn = P.logn; T.word_bits = P.word_bits; T.q = P.q; T.qinv_neg = P.qinv_neg;
   T.f = P.f; T.fs = P.fs; T.wf = P.wf; T.wfs = P.wfs; T.fw = fw; T.iw = iw;
   T.f4 = P.f4; T.f4s = P.f4s; T.wf4 = P.wf4; T.wf4s = P.wf4s;
+  T.f8 = P.f8; T.f8s = P.f8s; T.wf8 = P.wf8; T.wf8s = P.wf8s;
   T.fi = P.fi; T.fis = P.fis; T.wfi = P.wfi; T.wfis = P.wfis; T.r2 = P.r2;
   CK(hipDeviceGetAttribute(&T.cus, hipDeviceAttributeMultiprocessorCount, 0));
   CK(nttmul::launch_fill(a, b, P.logn, q, 0x4E54544D554Cull, 0, batch, io_bits, 0));
