@@ -88,3 +88,24 @@ def test_basemul_fold_bounds(q):
         r = (s2 + m * q) >> 32
         assert r < 2 * q
         assert r % q == (s * pow(2, -32, q)) % q
+
+
+@pytest.mark.parametrize("q", QS)
+def test_p3_halfway_fold_bounds(q):
+    """Arith32P3::basemul (8-coefficient blocks): four products, fold, four more products, fold,
+    Montgomery; arith_select.hpp p3_fold_ok admits q only when the halfway sum fits 64 bits."""
+    c32 = (1 << 32) % q
+    qneg = (-pow(q, -1, 1 << 32)) % (1 << 32)
+    half = 4 * (q - 1) ** 2
+    ok = ((half >> 32) * c32 + 0xFFFFFFFF + half) < M64
+    if not ok:
+        pytest.skip("q not eligible for D = 3 (the launcher keeps D = 2)")
+    rng = random.Random(q + 3)
+    for s1, s2 in [(half, half), (0, 0), (half, 0), (0, half)] + \
+            [(rng.randrange(half), rng.randrange(half)) for _ in range(2000)]:
+        s = (s1 >> 32) * c32 + (s1 & 0xFFFFFFFF) + s2
+        assert s < M64
+        f = (s >> 32) * c32 + (s & 0xFFFFFFFF)
+        m = ((f & 0xFFFFFFFF) * qneg) & 0xFFFFFFFF
+        r = (f + m * q) >> 32
+        assert r < 2 * q and r % q == ((s1 + s2) * pow(2, -32, q)) % q
