@@ -62,7 +62,9 @@ constexpr bool p_signed_fw_entry(int logn, uint32_t idx) {
 
 // Arith32P3 (base blocks of 8 coefficients, n = 4096 products only): each output sums eight
 // products of canonical values; the first four are folded by 2^32 mod q before the other four
-// are added, which keeps the sum below 2^64 only when 2^32 mod q is small enough
+// are added.  With q = x 2^31 the sum is below x^2 (2 - x) 2^64 when 2^32 mod q = 2^32 - 2q
+// (x > 2/3) and below x^2 (2 - 1.5 x) 2^64 when it is 2^32 - 3q, so every 2^30 < q < 2^31
+// qualifies; the check is kept so a change of range cannot silently overflow
 #ifndef NTTMUL_P3
 #define NTTMUL_P3 1
 #endif

@@ -458,10 +458,9 @@ struct Arith32P {
 // Arith32P with base blocks of 8 coefficients (D = 3): one butterfly stage fewer in each of the
 // three transforms for a base multiplication of 8 x 8 products per block.  Each output's eight
 // products of canonical values are summed in two halves: the first four (< 4 q^2) are folded by
-// 2^32 mod q before the other four are added, so the sum stays below 2^64 only when 2^32 mod q
-// is small (arith_select.hpp p3_fold_ok: q = 15 2^27 + 1 has 2^32 mod q = 2^28 - 2); the launcher
-// takes this class only for such q, and only at n = 4096 (the last register group must hold more
-// than 3 stages).
+// 2^32 mod q before the other four are added, which keeps the sum below 2^64 for every
+// 2^30 < q < 2^31 (arith_select.hpp p3_fold_ok, tests/test_plantard.py); the launcher takes this
+// class at n = 4096 only (the last register group must hold more than 3 stages).
 struct Arith32P3 : Arith32P {
   static constexpr int kBaseD = 3;
   template <int B, bool NEG, bool ZC = false>
