@@ -63,6 +63,10 @@
 #ifndef NTTMUL_PAD0
 #define NTTMUL_PAD0 1
 #endif
+// two-term pads at n = 512 / 1024 (Groups::PS2)
+#ifndef NTTMUL_PAD2
+#define NTTMUL_PAD2 1
+#endif
 // NTTMUL_SPLIT16 (column stages of the n = 65536 multi-pass product): arith_select.hpp
 #ifndef NTTMUL_ABL_NOLOAD
 #define NTTMUL_ABL_NOLOAD 0
@@ -141,13 +145,28 @@ struct Groups {
   // elements across the wave, which e + (e >> 4) 2-way conflicts (every 32 consecutive words span
   // 34); e + ((e >> (LOGS - 4)) << (LOGS - 8)) keeps those lanes on distinct banks and still
   // separates group 1's two 16-element halves.  Exchange 1 (groups 1 <-> 2) keeps e + (e >> 4).
+  // n = 1024 and 512 (one wave per product, three groups of 3-4 stages) take a second term,
+  // e + ((e >> s) << t) + ((e >> s2) << t2), found by the same census (tests/test_layout.py): the
+  // single-term pads left 32 extra cycles on each exchange at n = 1024 (PMC: 33 % of LDS cycles)
   static constexpr bool kPad0 = NTTMUL_PAD0 && LOGS >= 10 && G > 2;
-  static constexpr int PS(int x) { return x == 0 && kPad0 ? LOGS - 4 : 4; }
-  static constexpr int PT(int x) { return x == 0 && kPad0 ? LOGS - 8 : 0; }
+  static constexpr bool kPad2 = NTTMUL_PAD0 && NTTMUL_PAD2 && (LOGS == 10 || LOGS == 9);
+  static constexpr int PS(int x) {
+    return kPad2 ? (LOGS == 10 ? (x == 0 ? 6 : 4) : (x == 0 ? 5 : 4))
+                 : (x == 0 && kPad0 ? LOGS - 4 : 4);
+  }
+  static constexpr int PT(int x) {
+    return kPad2 ? (LOGS == 10 ? (x == 0 ? 3 : 1) : (x == 0 ? 0 : 1))
+                 : (x == 0 && kPad0 ? LOGS - 8 : 0);
+  }
+  static constexpr int PS2(int x) { return kPad2 ? (LOGS == 10 ? 8 : (x == 0 ? 7 : 8)) : 31; }
   template <int X>
-  static constexpr int padx(int e) { return e + ((e >> PS(X)) << PT(X)); }
+  static constexpr int padx(int e) { return e + ((e >> PS(X)) << PT(X)) + (e >> PS2(X)); }
   static constexpr int pad(int e) { return padx<1>(e); }
-  static constexpr int NP = N + N / 16;  // padded LDS words per polynomial (>= every padx)
+  // padded LDS words per polynomial (>= every padx + 1; the pads are increasing in e)
+  static constexpr int NP = (padx<0>(N - 1) > padx<1>(N - 1) ? padx<0>(N - 1) : padx<1>(N - 1)) + 1 >
+                                    N + N / 16
+                                ? (padx<0>(N - 1) > padx<1>(N - 1) ? padx<0>(N - 1) : padx<1>(N - 1)) + 1
+                                : N + N / 16;
 };
 
 template <int LOGS>
