@@ -85,6 +85,9 @@ def parse(argv=None):
                     help="alternate consecutive steps over this many HIP streams (default 1; 2 "
                          "overlaps one launch's tail with the next one's ramp: a C2-sized batch "
                          "is a single generation of workgroups)")
+    ap.add_argument("--power-seconds", type=float, default=4.0,
+                    help="after the timed region, keep stepping this long while amd-smi samples "
+                         "board power and clocks (rank 0 at N=1; 0 disables)")
     ap.add_argument("--dump-samples", default="",
                     help="write <prefix>.rank<r>.npz with sampled products of this rank's slice "
                          "(checked against the oracle by tests/test_gpu_parity.py)")
@@ -233,6 +236,115 @@ def buffer_sets(step_bytes: int, requested: int = 0) -> int:
     if requested > 0:
         return requested
     return -(-3 * IC_BYTES // step_bytes) if step_bytes <= IC_BYTES else 1
+
+
+def _num(x):
+    return x if isinstance(x, (int, float)) and not isinstance(x, bool) else None
+
+
+def power_reader(bdf: str, devno: int):
+    """(read, cap_w, index) over the amdsmi library in this process -- read-only queries through
+    the kernel driver, no child process -- or None when amdsmi is unavailable.  read() returns one
+    sample: socket power (W), shader clock (MHz), gfx activity (%), PPT (package power) limiter
+    state.  The GPU is matched by PCI address, else by index."""
+    try:
+        import amdsmi as S
+        S.amdsmi_init()
+        hs = S.amdsmi_get_processor_handles()
+    except Exception:  # no library, no driver access
+        return None
+    h, idx = None, None
+    for i, x in enumerate(hs):
+        try:
+            if bdf and str(S.amdsmi_get_gpu_device_bdf(x)).lower().startswith(bdf.lower()):
+                h, idx = x, i
+        except Exception:
+            continue
+    if h is None and devno < len(hs):
+        h, idx = hs[devno], devno
+    if h is None:
+        return None
+    cap = None
+    try:
+        c = _num(S.amdsmi_get_power_cap_info(h).get("power_cap"))
+        cap = c / 1e6 if c and c > 1e5 else c          # the library reports microwatts
+    except Exception:
+        pass
+
+    def read():
+        row = {}
+        try:
+            p = S.amdsmi_get_power_info(h)
+            row["w"] = next((_num(p.get(k)) for k in ("current_socket_power", "socket_power",
+                                                      "average_socket_power")
+                             if _num(p.get(k))), None)
+        except Exception:
+            row["w"] = None
+        try:
+            row["mhz"] = _num(S.amdsmi_get_clock_info(h, S.AmdSmiClkType.GFX).get("clk"))
+        except Exception:
+            row["mhz"] = None
+        try:
+            row["busy"] = _num(S.amdsmi_get_gpu_activity(h).get("gfx_activity"))
+        except Exception:
+            row["busy"] = None
+        try:
+            v = S.amdsmi_get_violation_status(h)
+            a = v.get("active_ppt_pwr")
+            row["ppt"] = a if isinstance(a, bool) else None
+            row["ppt_pct"] = _num(v.get("per_ppt_pwr"))
+        except Exception:
+            row["ppt"], row["ppt_pct"] = None, None
+        return row
+
+    return read, cap, idx
+
+
+def power_probe(step, sync, seconds: float, reader):
+    """Board power while the timed workload keeps running (the product kernels are
+    bound by the package power cap).  After the timed region, extra steps run for `seconds` while
+    a thread samples `reader` (power_reader) every 0.2 s; reports the median socket power, the cap,
+    the median shader clock and how many busy samples had the PPT limiter engaged."""
+    import statistics
+    import threading
+    if reader is None:
+        return None
+    read, cap, idx = reader
+    done = threading.Event()
+    rows = []
+
+    def sample():
+        while not done.wait(0.2):
+            rows.append(read())
+
+    th = threading.Thread(target=sample, daemon=True)
+    t_end = time.perf_counter() + seconds
+    th.start()
+    while time.perf_counter() < t_end:
+        for _ in range(32):
+            step()
+        sync()
+    done.set()
+    th.join(timeout=30)
+    busy = [r for r in rows if (r.get("busy") or 0) >= 90 and r.get("w")]
+    out = {"socket_power_cap_w": cap, "samples": len(rows), "busy_samples": len(busy),
+           "amd_smi_gpu": idx,
+           "source": f"amdsmi library (in process) sampled every 0.2 s during {seconds:g} s of "
+                     "further steps after the timed region; medians over gfx-busy samples"}
+    if busy:
+        out["socket_power_w_median"] = statistics.median(r["w"] for r in busy)
+        clk = [r["mhz"] for r in busy if r.get("mhz")]
+        if clk:
+            out["gfx_clock_mhz_median"] = statistics.median(clk)
+        ppt = [r["ppt"] for r in busy if r.get("ppt") is not None]
+        if ppt:
+            out["ppt_limiter_active"] = f"{sum(ppt)}/{len(ppt)}"
+        pct = [r["ppt_pct"] for r in busy if r.get("ppt_pct") is not None]
+        if pct:
+            out["ppt_violation_pct_median"] = statistics.median(pct)
+    return out
+
+
 MAX_CLOCK_GHZ = 2.4         # MI355X max engine clock (MI355X_MICROARCH.md)
 SIMDS = 1024                # 256 CUs x 4 SIMDs
 
@@ -383,6 +495,18 @@ def main(argv=None):
                 "source": f"profiles/valu_bound.json (code object {co}): the ISA listing priced "
                           "at measured issue costs, at the 2.4 GHz max clock; implied_clock_ghz "
                           "= the clock at which the kernel would run exactly at that issue bound"}
+        if world == 1 and args.power_seconds > 0:
+            try:
+                props = torch.cuda.get_device_properties(dev)
+                bdf = (f"{props.pci_domain_id:04x}:{props.pci_bus_id:02x}:"
+                       f"{props.pci_device_id:02x}")
+            except AttributeError:
+                bdf = ""
+            try:
+                line["power"] = power_probe(step, lambda: torch.cuda.synchronize(dev),
+                                            args.power_seconds, power_reader(bdf, devno))
+            except Exception as e:  # reported evidence, never required
+                line["power"] = {"error": str(e)}
         if args.host_io:
             a, b, _ = sets[0]
             line["host_io"] = host_io(ctx, a, b, count, n, wb)

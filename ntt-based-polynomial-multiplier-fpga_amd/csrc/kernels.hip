@@ -840,7 +840,10 @@ static hipError_t polymul_io(const LaunchTables &T, const void *a, const void *b
 
 hipError_t launch_polymul(const LaunchTables &T, const void *a, const void *b, void *c,
                           size_t batch, int io_bits, void **scr, hipStream_t s) {
-#if NTTMUL_KBENCH_LITE  // tools/kbench quick builds: 32-bit words, q < 2^31, n <= 4096 only
+#if NTTMUL_KBENCH_LITE == 2  // tools/kbench C5 builds: 64-bit words, n = 65536 only
+  if (T.word_bits != 64 || T.logn != 16 || io_bits != 64) return hipErrorNotSupported;
+  return multipass_l1<Arith64, uint64_t, 4>(T, a, b, c, batch, scr[0], scr[1], scr[2], s);
+#elif NTTMUL_KBENCH_LITE  // tools/kbench quick builds: 32-bit words, q < 2^31, n <= 4096 only
   if (T.word_bits != 32 || T.q >= (1ull << 31) || T.logn > 12 || io_bits != 32) return hipErrorNotSupported;
   switch (a32_kind(T.q)) {
     case A32Kind::Harvey: return fused<Arith32H, uint32_t>(T, a, b, c, batch, s);

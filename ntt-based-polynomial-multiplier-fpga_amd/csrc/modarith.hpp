@@ -572,6 +572,10 @@ struct Arith32W {
 #ifndef NTTMUL_A64_V2
 #define NTTMUL_A64_V2 1
 #endif
+// high product through the carry-out of v_mad_u64_u32 (Arith64::mulhi64; tools/kbench A/B)
+#ifndef NTTMUL_A64_MADC
+#define NTTMUL_A64_MADC 1
+#endif
 struct Arith64 {
   using word = uint64_t;
   static constexpr int kBits = 64;
@@ -596,13 +600,35 @@ struct Arith64 {
     return __builtin_sub_overflow(x, m, &d) ? x : d;
 #endif
   }
-  // high 64 bits of the 128-bit product x * s, from four 32x32 products
+  // high 64 bits of the 128-bit product x * s, from four 32x32 products.  MADC: the carry-out
+  // form below (the butterflies' Shoup products only: in the base multiplication's loops the asm
+  // blocks cost the full unroll, and the row kernel fell back to scratch-indexed arrays)
+  template <bool MADC = false>
   __device__ __forceinline__ static uint64_t mulhi64(uint64_t x, uint64_t s) {
 #if NTTMUL_A64_PLAIN
     return __umul64hi(x, s);
 #else
     const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
     const uint32_t sl = (uint32_t)s, sh = (uint32_t)(s >> 32);
+#if NTTMUL_A64_MADC
+    if constexpr (MADC) {
+    // x s = xh sh 2^64 + (xh sl + t) 2^32 + lo32(xl sl) with t = xl sh + hi32(xl sl) < 2^64.
+    // xh sl + t can reach 2^65: the carry-out of v_mad_u64_u32 (its SGPR-pair destination, which
+    // the compiler's own multiply-adds leave dead) supplies bit 64, so the high product is
+    // xh sh + (carry 2^32 + hi32(u)) with no zero-extension moves: 6 VALU instead of 8.
+    // s_nop 1: two wait states between the VALU write of the carry mask and its VALU read
+    // (the hazard the compiler covers for its own carry chains; it does not see inside asm).
+    const uint64_t t = (uint64_t)xl * sh + __umulhi(xl, sl);
+    uint64_t u, cc;
+    uint32_t c;
+    asm("v_mad_u64_u32 %0, %2, %3, %4, %5\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %1, 0, 1, %2"
+        : "=&v"(u), "=v"(c), "=&s"(cc)
+        : "v"(xh), "v"(sl), "v"(t));
+    return (uint64_t)xh * sh + ((u >> 32) | ((uint64_t)c << 32));
+    }
+#endif
 #if NTTMUL_A64_V2
     const uint64_t p00 = (uint64_t)xl * sl;
     const uint64_t t = (uint64_t)xl * sh + (p00 >> 32);
@@ -628,8 +654,9 @@ struct Arith64 {
 #endif
   }
   // x * w mod q in [0, 2q) for any 64-bit x (Shoup, w' = floor(w 2^64 / q))
+  template <bool MADC = true>
   __device__ __forceinline__ uint64_t shoup(uint64_t x, uint64_t w, uint64_t ws) const {
-    const uint64_t qh = mulhi64(x, ws);
+    const uint64_t qh = mulhi64<MADC>(x, ws);
 #if NTTMUL_A64_V2
     // lo64(x w) - lo64(qh q) in one pass: D = xl wl + hl (2^32 - ql) carries the low word and a
     // high word off by +hl, which the complemented constants absorb (2 v_mad_u64_u32,
@@ -724,7 +751,7 @@ struct Arith64 {
       br[i] = canon(b[i]);
     }
 #pragma unroll
-    for (int i = 1; i < B; i++) bz[i] = csub(shoup(b[i], w, ws), q);
+    for (int i = 1; i < B; i++) bz[i] = csub(shoup<false>(b[i], w, ws), q);
 #pragma unroll
     for (int k = 0; k < B; k++) {
       unsigned __int128 s = 0;

@@ -75,3 +75,23 @@ def test_profile_lookup_fails_closed(tmp_path, monkeypatch):
     t, src = bench.load_traffic(4096, 2013265921, 65536, "bbbb")   # another build
     assert t is None and "bbbb" in src
     assert bench.load_valu_bound(4096, 2013265921, "aaaa") is None  # no file: None
+
+
+def test_power_probe_summary():
+    """bench.power_probe: medians over the gfx-busy samples, the cap, the PPT-limiter count, and
+    None without a reader (amdsmi replaced by a canned sampler)."""
+    it = iter(range(10 ** 6))
+
+    def read():
+        i = next(it)
+        return {"w": 1399 if i % 2 else 1397, "mhz": 1900 + (i % 3) * 50, "busy": 100 if i else 0,
+                "ppt": True, "ppt_pct": 100}
+
+    steps = []
+    out = bench.power_probe(lambda: steps.append(1), lambda: None, 0.7, (read, 1400.0, 3))
+    assert steps and out["amd_smi_gpu"] == 3 and out["socket_power_cap_w"] == 1400.0
+    assert out["busy_samples"] == out["samples"] - 1 >= 1
+    assert out["socket_power_w_median"] in (1397, 1398, 1399)
+    assert out["ppt_limiter_active"] == f"{out['busy_samples']}/{out['busy_samples']}"
+    assert bench.power_probe(lambda: None, lambda: None, 0.01, None) is None
+    assert bench.power_reader("", 0) is None or callable(bench.power_reader("", 0)[0])
