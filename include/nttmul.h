@@ -86,11 +86,21 @@ int nttmul_multiply_u32(nttmul_ctx *ctx, uint32_t *c, const uint32_t *a, const u
 int nttmul_multiply_u64(nttmul_ctx *ctx, uint64_t *c, const uint64_t *a, const uint64_t *b);
 
 /* batch of independent products; host buffers [batch][n], row-major.  Split over the context's
- * devices in contiguous slices (no inter-device traffic). */
+ * devices in contiguous slices (no inter-device traffic).  Buffers in pageable memory are staged
+ * through the context's pinned buffers by host threads (the bound of this path); when a, b and c
+ * all lie in page-locked memory (nttmul_host_alloc, or hipHostMalloc / hipHostRegister by the
+ * caller) the copy engines DMA the chunks straight from and to them, as the FPGA communicator's
+ * PCIE_DmaWrite / PCIE_DmaRead did from its own buffers (NTT_PCIECommunicationv2.c:164-229). */
 int nttmul_multiply_batch_u32(nttmul_ctx *ctx, uint32_t *c, const uint32_t *a, const uint32_t *b,
                               size_t batch);
 int nttmul_multiply_batch_u64(nttmul_ctx *ctx, uint64_t *c, const uint64_t *a, const uint64_t *b,
                               size_t batch);
+
+/* Page-locked host memory for the host-buffer calls above (the DMA buffers of the FPGA flow,
+ * NTT_PCIECommunicationv2.c:164-229 PCIE_DmaWrite/DmaRead): *p = NULL and NTTMUL_ENOMEM on
+ * failure, NTTMUL_ENODEV without a device.  Free with nttmul_host_free. */
+int nttmul_host_alloc(void **p, size_t bytes);
+void nttmul_host_free(void *p);
 
 /* Device-resident batch on HIP device `dev` (must be one of the context's devices), enqueued on
  * `stream` (a hipStream_t of that device; NULL is the device's null stream, as everywhere in HIP).

@@ -409,6 +409,21 @@ int ensure_slots(nttmul_ctx *ctx, DevState &d, size_t bytes) {
   return NTTMUL_OK;
 }
 
+// True when [p, p + bytes) lies in page-locked host memory the copy engines can DMA directly
+// (hipHostMalloc'd or hipHostRegister'ed; both ends checked, the range may span two such blocks).
+bool host_pinned(const void *p, size_t bytes) {
+  if (!p || !bytes) return false;
+  for (const void *q : {p, (const void *)((const char *)p + bytes - 1)}) {
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, q) != hipSuccess) {
+      (void)hipGetLastError();  // pageable memory: the query fails, clear the sticky error
+      return false;
+    }
+    if (at.type != hipMemoryTypeHost) return false;
+  }
+  return true;
+}
+
 // Host-buffer path (the FPGA transaction: mode 1/2 DMA in, mode 3, DMA out).  Each device's
 // contiguous slice streams through kSlots pipeline slots in chunks: the host copies
 // chunk j into pinned staging while the GPU runs H2D -> kernel -> D2H of chunks j-1, j-2 on the
@@ -447,13 +462,18 @@ int run_host(nttmul_ctx *ctx, int op, void *c, const void *a, const void *b, siz
     }
     p0 = p1;
   }
+  // page-locked caller buffers: DMA straight from / to them, no staging copies (retire only
+  // waits, and only at the end: a slot's stream orders its own chunks)
+  const size_t total = batch * pbytes;
+  const bool direct = host_pinned(a, total) && (!two || host_pinned(b, total)) &&
+                      host_pinned(c, total);
   auto retire = [&](int i, int s) -> int {
     DevState &d = ctx->dev[i];
     Pending &pd = job[i].slot[s];
     if (!pd.busy) return NTTMUL_OK;
     HIP_TRY(ctx, hipSetDevice(d.id));
     HIP_TRY(ctx, hipStreamSynchronize(d.xs[s]));
-    pcopy((char *)c + pd.off, d.pin[s][2], pd.bytes);
+    if (!direct) pcopy((char *)c + pd.off, d.pin[s][2], pd.bytes);
     pd.busy = false;
     return NTTMUL_OK;
   };
@@ -466,9 +486,32 @@ int run_host(nttmul_ctx *ctx, int op, void *c, const void *a, const void *b, siz
       more = true;
       DevState &d = ctx->dev[i];
       const int s = (int)(J.k++ % kSlots);
-      if ((st = retire(i, s))) break;
       const size_t cnt = std::min(chunk, J.end - J.next);
       const size_t off = J.next * pbytes, bytes = cnt * pbytes;
+      if (direct) {
+        HIP_TRY(ctx, hipSetDevice(d.id));
+        hipError_t e = hipMemcpyAsync(d.dbuf[s][0], (const char *)a + off, bytes,
+                                      hipMemcpyHostToDevice, d.xs[s]);
+        if (e == hipSuccess && two)
+          e = hipMemcpyAsync(d.dbuf[s][1], (const char *)b + off, bytes, hipMemcpyHostToDevice,
+                             d.xs[s]);
+        if (e != hipSuccess) {
+          st = fail(ctx, e, "hipMemcpyAsync H2D");
+          break;
+        }
+        if ((st = run_device(ctx, d, d.sscr[s], op, d.dbuf[s][2], d.dbuf[s][0], d.dbuf[s][1],
+                             cnt, io_bits, d.xs[s])))
+          break;
+        e = hipMemcpyAsync((char *)c + off, d.dbuf[s][2], bytes, hipMemcpyDeviceToHost, d.xs[s]);
+        if (e != hipSuccess) {
+          st = fail(ctx, e, "hipMemcpyAsync D2H");
+          break;
+        }
+        J.slot[s] = Pending{true, off, bytes};
+        J.next += cnt;
+        continue;
+      }
+      if ((st = retire(i, s))) break;
       pcopy(d.pin[s][0], (const char *)a + off, bytes);
       if (two) pcopy(d.pin[s][1], (const char *)b + off, bytes);
       if (bytes <= zero_copy && ctx->plan.logn <= 12) {
@@ -527,6 +570,26 @@ const char *nttmul_strerror(int status) {
 }
 
 const char *nttmul_last_error(const nttmul_ctx *ctx) { return ctx ? ctx->err : ""; }
+
+int nttmul_host_alloc(void **p, size_t bytes) {
+  if (!p) return NTTMUL_EINVAL;
+  *p = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
+    (void)hipGetLastError();
+    return NTTMUL_ENODEV;
+  }
+  if (hipHostMalloc(p, bytes ? bytes : 1, hipHostMallocPortable) != hipSuccess) {
+    (void)hipGetLastError();
+    *p = nullptr;
+    return NTTMUL_ENOMEM;
+  }
+  return NTTMUL_OK;
+}
+
+void nttmul_host_free(void *p) {
+  if (p) (void)hipHostFree(p);
+}
 
 int nttmul_create_ex(nttmul_ctx **out, const nttmul_params *prm) {
   if (!out || !prm) return NTTMUL_EINVAL;

@@ -244,14 +244,19 @@ class Context:
     def io_dtype(self):
         return np.uint32 if self.q < (1 << 32) else np.uint64
 
-    def multiply(self, a, b, dtype=None) -> np.ndarray:
-        """c = a * b mod (x^n + 1, q) for host arrays of shape [n] or [batch, n]."""
+    def multiply(self, a, b, dtype=None, out=None) -> np.ndarray:
+        """c = a * b mod (x^n + 1, q) for host arrays of shape [n] or [batch, n].  `out`: the
+        result array (same shape and dtype); with a, b and out in page-locked memory
+        (host_empty) the library DMAs straight from and to them instead of staging."""
         dtype = dtype or self.io_dtype
         a = np.ascontiguousarray(a, dtype=dtype)
         b = np.ascontiguousarray(b, dtype=dtype)
         if a.shape != b.shape or a.shape[-1] != self.n:
             raise ValueError("a and b must both have shape [..., n]")
-        c = np.empty_like(a)
+        if out is not None and (out.shape != a.shape or out.dtype != a.dtype
+                                or not out.flags.c_contiguous):
+            raise ValueError("out must be a C-contiguous array of a's shape and dtype")
+        c = np.empty_like(a) if out is None else out
         batch = a.size // self.n
         fn = self._lib.nttmul_multiply_batch_u32 if dtype == np.uint32 else self._lib.nttmul_multiply_batch_u64
         self._check(fn(self._h, c.ctypes.data, a.ctypes.data, b.ctypes.data, batch))
@@ -347,6 +352,37 @@ class Context:
 
 
 # ---- planner API ------------------------------------------------------------
+
+class _HostBlock:
+    """Owner of one nttmul_host_alloc block (freed with the last numpy view of it)."""
+
+    def __init__(self, nbytes: int):
+        lib = load_library()
+        lib.nttmul_host_alloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+        lib.nttmul_host_free.argtypes = [ctypes.c_void_p]
+        lib.nttmul_host_free.restype = None
+        p = ctypes.c_void_p()
+        st = lib.nttmul_host_alloc(ctypes.byref(p), nbytes)
+        if st != NTTMUL_OK:
+            raise NttmulError(st, strerror(st))
+        self._lib, self.ptr, self.nbytes = lib, p.value, nbytes
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            self._lib.nttmul_host_free(self.ptr)
+            self.ptr = None
+
+
+def host_empty(shape, dtype) -> np.ndarray:
+    """Uninitialised numpy array in page-locked host memory (nttmul_host_alloc): host-buffer
+    calls whose operands all live in such arrays DMA directly, without the staging copy."""
+    dtype = np.dtype(dtype)
+    count = int(np.prod(shape))
+    blk = _HostBlock(max(1, count * dtype.itemsize))
+    buf = (ctypes.c_char * blk.nbytes).from_address(blk.ptr)
+    buf._nttmul_block = blk                      # the ctypes buffer keeps the block alive
+    return np.frombuffer(buf, dtype=dtype, count=count).reshape(shape)
+
 
 def is_prime(q: int) -> bool:
     return bool(load_library().nttmul_is_prime(q))

@@ -16,7 +16,8 @@ def test_library_exports_every_declared_symbol():
                 "nttmul_last_error", "nttmul_get_info", "nttmul_multiply_u32",
                 "nttmul_multiply_u64", "nttmul_multiply_batch_u32", "nttmul_multiply_batch_u64",
                 "nttmul_multiply_batch_device", "nttmul_fill_random_device", "ntt256_product1",
-                "ntt256_product4", "ntt_red256_product1", "ntt_red256_product4"}
+                "ntt256_product4", "ntt_red256_product1", "ntt_red256_product4",
+                "nttmul_host_alloc", "nttmul_host_free"}
     assert expected <= set(syms), set(expected) - set(syms)
     for s in syms:
         assert hasattr(lib, s), s
@@ -49,4 +50,12 @@ def test_no_gpu_fails_loudly():
     """Without a HIP device there is no silent CPU fallback: create returns NTTMUL_ENODEV."""
     with pytest.raises(nttmul.NttmulError) as ei:
         nttmul.Context(4096, 2013265921)
+    assert ei.value.status == nttmul.NTTMUL_ENODEV
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="checks the no-GPU behaviour")
+def test_no_device_host_alloc():
+    """nttmul_host_alloc without a device: NTTMUL_ENODEV and a NULL pointer, no fallback."""
+    with pytest.raises(nttmul.NttmulError) as ei:
+        nttmul.host_empty((4, 16), "uint32")
     assert ei.value.status == nttmul.NTTMUL_ENODEV

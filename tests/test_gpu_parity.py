@@ -409,6 +409,25 @@ def test_host_path_pipeline(n, q, batch, torch_cuda):
     assert np.array_equal(ctx.inverse(fa).astype(np.uint64), a)
 
 
+@pytest.mark.parametrize("n,q,batch", [(4096, Q31, 1537), (1024, Q62, 1100), (65536, Q62, 20)])
+def test_host_path_pinned_direct(n, q, batch, torch_cuda):
+    """Page-locked operands (nttmul.host_empty = nttmul_host_alloc) take the direct-DMA branch of
+    run_host (no staging copies; several chunks over the slots): every product equals the
+    oracle's and the pageable path's; mixing pinned and pageable buffers takes the staged path."""
+    ctx = _ctx(n, q)
+    a, b = O.fill_inputs(n, q, 23, batch)
+    dt = np.uint32 if q < (1 << 32) else np.uint64
+    ap, bp, cp = (nttmul.host_empty((batch, n), dt) for _ in range(3))
+    ap[...] = a
+    bp[...] = b
+    cp[...] = 0
+    assert ctx.multiply(ap, bp, out=cp) is cp
+    ref = O.Plan(n, q).product_batch(a, b)[0].reshape(batch, n)
+    assert np.array_equal(cp.astype(np.uint64), ref)
+    mixed = ctx.multiply(ap, b.astype(dt))            # c pageable: staged
+    assert np.array_equal(mixed.astype(np.uint64), ref)
+
+
 # ---------------------------------------------------------------------------------------------
 # The reference's whole transform wrapper set (NTT/ntt256.h:20-69) and its general form
 # ---------------------------------------------------------------------------------------------
