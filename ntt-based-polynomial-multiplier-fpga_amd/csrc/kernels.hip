@@ -33,6 +33,18 @@
 #ifndef NTTMUL_LDS_REGIONS
 #define NTTMUL_LDS_REGIONS 1
 #endif
+// a, b, c streams of the one-product-per-block u32 products (n = 4096, 1024) as buffer loads /
+// stores on a block-uniform descriptor with cache-policy bits aux = NTTMUL_CPOL (1 sc0, 2 nt,
+// 16 sc1; -1: global loads as below).  C3 kbench A/B (profiles/r2/cpol_ab.txt, identical
+// checksums): nt -1.2 % against the global nt loads (the 32-bit voffset form drops the 64-bit
+// address adds: 1,940 VALU per wave instead of 1,951); nt with sc0 / sc1 the same as nt alone;
+// plain (0) +0.3 %, sc1 alone +0.1 %
+#ifndef NTTMUL_CPOL
+#define NTTMUL_CPOL 2
+#endif
+#ifndef NTTMUL_CPOL_ST
+#define NTTMUL_CPOL_ST NTTMUL_CPOL
+#endif
 // non-temporal loads/stores of the coefficient streams in k_rows
 #ifndef NTTMUL_NT
 #define NTTMUL_NT 1
@@ -512,6 +524,10 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
 #endif
 
   W x[16], y[16];
+  // NTTMUL_CPOL >= 0: a, b, c of a one-product-per-block u32 product through buffer loads /
+  // stores (descriptor from block-uniform values, 32-bit per-lane offsets, nt by default)
+  constexpr bool kCpol = NTTMUL_CPOL >= 0 && PB == 1 && L1 == 0 && sizeof(W) == 4 &&
+                         sizeof(TIn) == 4 && sizeof(TOut) == 4;
 #if NTTMUL_ABL_NOLOAD
 #pragma unroll
   for (int k = 0; k < 16; k++) {
@@ -519,6 +535,19 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
     y[k] = (W)(j * 7 + k * 3 + u);
   }
 #else
+  if constexpr (kCpol) {
+    const size_t ub = live ? (size_t)blockIdx.x : 0;
+    const auto ra = __builtin_amdgcn_make_buffer_rsrc((void *)(a + ub * N), 0, N * 4, 0x00020000);
+    const auto rb = __builtin_amdgcn_make_buffer_rsrc((void *)(b + ub * N), 0, N * 4, 0x00020000);
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const int off = (Gr::base(0, j) + Gr::off(0, k)) * 4;
+      x[k] = (W)__builtin_amdgcn_raw_buffer_load_b32(ra, off, 0, NTTMUL_CPOL < 0 ? 0 : NTTMUL_CPOL);
+      y[k] = (W)__builtin_amdgcn_raw_buffer_load_b32(rb, off, 0, NTTMUL_CPOL < 0 ? 0 : NTTMUL_CPOL);
+    }
+  } else
+#endif
+#if !NTTMUL_ABL_NOLOAD
 #pragma unroll
   for (int k = 0; k < 16; k++) {
     x[k] = to_word<W>(ld_stream<kNT>(a + base_r + Gr::off(0, k)));
@@ -538,6 +567,21 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
   if (acc == (W)0x5A5A5A5A && live) c[base_g] = (TOut)acc;
   return;
 #endif
+  if constexpr (kCpol) {
+    if (live) {
+      const auto rc = __builtin_amdgcn_make_buffer_rsrc((void *)(c + (size_t)blockIdx.x * N), 0,
+                                                        N * 4, 0x00020000);
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        W v = x[k];
+        if (!A::kInvCanonical) v = P.ar.canon(v);
+        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, rc,
+                                              (Gr::base(0, j) + Gr::off(0, k)) * 4, 0,
+                                              NTTMUL_CPOL_ST < 0 ? 0 : NTTMUL_CPOL_ST);
+      }
+    }
+    return;
+  }
   if (live) {
 #pragma unroll
     for (int k = 0; k < 16; k++) {
