@@ -227,6 +227,21 @@ __device__ __forceinline__ void st_stream(T *p, T v) {
     *p = v;
 }
 
+// Buffer-resource streams (NTTMUL_CPOL): a descriptor over one block-uniform span of words and
+// 32-bit per-lane byte offsets; AUX = the cache-policy bits of the load / store
+template <class T>
+__device__ __forceinline__ auto span_rsrc(const T *p, size_t words) {
+  return __builtin_amdgcn_make_buffer_rsrc((void *)p, 0, (int)(words * sizeof(T)), 0x00020000);
+}
+template <int AUX, class R>
+__device__ __forceinline__ uint32_t buf_ld32(R r, int byte_off) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, AUX);
+}
+template <int AUX, class R>
+__device__ __forceinline__ void buf_st32(R r, int byte_off, uint32_t v) {
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, byte_off, 0, AUX);
+}
+
 // Forward CT stages of group g on NPOLY (1 or 2) polynomials (same twiddles).  SKIP: leave out
 // the last SKIP stages of the group (the incomplete transform of the product kernel, see
 // base_mult); the twiddles of the last stage performed are kept in zw[X register].
@@ -526,8 +541,12 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
   W x[16], y[16];
   // NTTMUL_CPOL >= 0: a, b, c of a one-product-per-block u32 product through buffer loads /
   // stores (descriptor from block-uniform values, 32-bit per-lane offsets, nt by default)
+  // (64-bit words and the multi-pass passes keep global loads: the same form measured +0.8 % at
+  // C5, its row pass at 131 VGPRs instead of 126)
   constexpr bool kCpol = NTTMUL_CPOL >= 0 && PB == 1 && L1 == 0 && sizeof(W) == 4 &&
                          sizeof(TIn) == 4 && sizeof(TOut) == 4;
+  constexpr int kAux = NTTMUL_CPOL < 0 ? 0 : NTTMUL_CPOL;
+  constexpr int kAuxSt = NTTMUL_CPOL_ST < 0 ? 0 : NTTMUL_CPOL_ST;
 #if NTTMUL_ABL_NOLOAD
 #pragma unroll
   for (int k = 0; k < 16; k++) {
@@ -537,13 +556,12 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
 #else
   if constexpr (kCpol) {
     const size_t ub = live ? (size_t)blockIdx.x : 0;
-    const auto ra = __builtin_amdgcn_make_buffer_rsrc((void *)(a + ub * N), 0, N * 4, 0x00020000);
-    const auto rb = __builtin_amdgcn_make_buffer_rsrc((void *)(b + ub * N), 0, N * 4, 0x00020000);
+    const auto ra = span_rsrc(a + ub * N, N), rb = span_rsrc(b + ub * N, N);
 #pragma unroll
     for (int k = 0; k < 16; k++) {
       const int off = (Gr::base(0, j) + Gr::off(0, k)) * 4;
-      x[k] = (W)__builtin_amdgcn_raw_buffer_load_b32(ra, off, 0, NTTMUL_CPOL < 0 ? 0 : NTTMUL_CPOL);
-      y[k] = (W)__builtin_amdgcn_raw_buffer_load_b32(rb, off, 0, NTTMUL_CPOL < 0 ? 0 : NTTMUL_CPOL);
+      x[k] = (W)buf_ld32<kAux>(ra, off);
+      y[k] = (W)buf_ld32<kAux>(rb, off);
     }
   } else
 #endif
@@ -569,15 +587,12 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
 #endif
   if constexpr (kCpol) {
     if (live) {
-      const auto rc = __builtin_amdgcn_make_buffer_rsrc((void *)(c + (size_t)blockIdx.x * N), 0,
-                                                        N * 4, 0x00020000);
+      const auto rc = span_rsrc(c + (size_t)blockIdx.x * N, N);
 #pragma unroll
       for (int k = 0; k < 16; k++) {
         W v = x[k];
         if (!A::kInvCanonical) v = P.ar.canon(v);
-        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, rc,
-                                              (Gr::base(0, j) + Gr::off(0, k)) * 4, 0,
-                                              NTTMUL_CPOL_ST < 0 ? 0 : NTTMUL_CPOL_ST);
+        buf_st32<kAuxSt>(rc, (Gr::base(0, j) + Gr::off(0, k)) * 4, (uint32_t)v);
       }
     }
     return;
