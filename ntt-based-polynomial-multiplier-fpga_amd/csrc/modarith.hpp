@@ -572,6 +572,12 @@ struct Arith32W {
 #ifndef NTTMUL_A64_V2
 #define NTTMUL_A64_V2 1
 #endif
+// base multiplication sums from 31-bit limb products (Arith64::basemul): -3.6 % VALU in the C5
+// row pass (the 128-bit carries and moves go; the 16 multiply-adds per output stay) but C5 time
+// unchanged at the power cap (profiles/r2/c5_limb_ab.txt, identical checksums): off
+#ifndef NTTMUL_A64_LIMB
+#define NTTMUL_A64_LIMB 0
+#endif
 // high product through the carry-out of v_mad_u64_u32 (Arith64::mulhi64; tools/kbench A/B)
 #ifndef NTTMUL_A64_MADC
 #define NTTMUL_A64_MADC 1
@@ -752,12 +758,41 @@ struct Arith64 {
     }
 #pragma unroll
     for (int i = 1; i < B; i++) bz[i] = csub(shoup<false>(b[i], w, ws), q);
+#if NTTMUL_A64_LIMB
+    // 31-bit limbs: x = xh 2^31 + xl (x < q < 2^62, so both limbs < 2^31).  Each limb product is
+    // below 2^62, so the four products of one output sum in a 64-bit accumulator per limb pair
+    // with chained v_mad_u64_u32 and no carries (4 instructions per 64 x 64 product instead of
+    // ~15 for the 128-bit product and accumulation); the 128-bit sum is assembled once per output.
+    uint32_t al[B], ah[B], bl[B], bh[B], zl[B], zh[B];
+#pragma unroll
+    for (int i = 0; i < B; i++) {
+      al[i] = (uint32_t)ar[i] & 0x7FFFFFFFu, ah[i] = (uint32_t)(ar[i] >> 31);
+      bl[i] = (uint32_t)br[i] & 0x7FFFFFFFu, bh[i] = (uint32_t)(br[i] >> 31);
+      if (i > 0) zl[i] = (uint32_t)bz[i] & 0x7FFFFFFFu, zh[i] = (uint32_t)(bz[i] >> 31);
+    }
+#endif
 #pragma unroll
     for (int k = 0; k < B; k++) {
+#if NTTMUL_A64_LIMB
+      uint64_t ll = 0, lh = 0, hl = 0, hh = 0;
+#pragma unroll
+      for (int i = 0; i < B; i++) {
+        const uint32_t yl = i <= k ? bl[k - i] : zl[B + k - i];
+        const uint32_t yh = i <= k ? bh[k - i] : zh[B + k - i];
+        ll += (uint64_t)al[i] * yl;
+        lh += (uint64_t)al[i] * yh;
+        hl += (uint64_t)ah[i] * yl;
+        hh += (uint64_t)ah[i] * yh;
+      }
+      const unsigned __int128 s = (unsigned __int128)ll +
+                                  (((unsigned __int128)lh + hl) << 31) +
+                                  ((unsigned __int128)hh << 62);
+#else
       unsigned __int128 s = 0;
 #pragma unroll
       for (int i = 0; i < B; i++)
         s += (unsigned __int128)ar[i] * (i <= k ? br[k - i] : bz[B + k - i]);
+#endif
       const uint64_t lo = (uint64_t)s, hi = (uint64_t)(s >> 64);
       const uint64_t m = lo * qinv_neg;
       // lo + lo64(m q) = 0 mod 2^64: its carry is (lo != 0)
