@@ -321,7 +321,7 @@ def power_reader(bdf: str, devno: int):
     return read, cap, idx
 
 
-def power_probe(step, sync, seconds: float, reader):
+def power_probe(step, sync, seconds: float, reader, units_per_step: int = 0):
     """Board power while the timed workload keeps running (the product kernels are
     bound by the package power cap).  After the timed region, extra steps run for `seconds` while
     a thread samples `reader` (power_reader) every 0.2 s; reports the median socket power, the cap,
@@ -339,12 +339,16 @@ def power_probe(step, sync, seconds: float, reader):
             rows.append(read())
 
     th = threading.Thread(target=sample, daemon=True)
-    t_end = time.perf_counter() + seconds
+    t0 = time.perf_counter()
+    t_end = t0 + seconds
+    nsteps = 0
     th.start()
     while time.perf_counter() < t_end:
         for _ in range(32):
             step()
         sync()
+        nsteps += 32
+    elapsed = time.perf_counter() - t0
     done.set()
     th.join(timeout=30)
     busy = [r for r in rows if (r.get("busy") or 0) >= 90 and r.get("w")]
@@ -354,6 +358,10 @@ def power_probe(step, sync, seconds: float, reader):
                      "further steps after the timed region; medians over gfx-busy samples"}
     if busy:
         out["socket_power_w_median"] = statistics.median(r["w"] for r in busy)
+        if units_per_step:  # board energy per unit of work at the rate of these extra steps
+            rate = units_per_step * nsteps / elapsed
+            out["rate_during_probe"] = rate
+            out["board_uj_per_unit"] = out["socket_power_w_median"] / rate * 1e6
         clk = [r["mhz"] for r in busy if r.get("mhz")]
         if clk:
             out["gfx_clock_mhz_median"] = statistics.median(clk)
@@ -525,7 +533,8 @@ def main(argv=None):
                 bdf = ""
             try:
                 line["power"] = power_probe(step, lambda: torch.cuda.synchronize(dev),
-                                            args.power_seconds, power_reader(bdf, devno))
+                                            args.power_seconds, power_reader(bdf, devno),
+                                            units_per_step=count)
             except Exception as e:  # reported evidence, never required
                 line["power"] = {"error": str(e)}
         if args.host_io:

@@ -88,7 +88,10 @@ def test_power_probe_summary():
                 "ppt": True, "ppt_pct": 100}
 
     steps = []
-    out = bench.power_probe(lambda: steps.append(1), lambda: None, 0.7, (read, 1400.0, 3))
+    out = bench.power_probe(lambda: steps.append(1), lambda: None, 0.7, (read, 1400.0, 3),
+                            units_per_step=1000)
+    assert out["board_uj_per_unit"] == pytest.approx(
+        out["socket_power_w_median"] / out["rate_during_probe"] * 1e6)
     assert steps and out["amd_smi_gpu"] == 3 and out["socket_power_cap_w"] == 1400.0
     assert out["busy_samples"] == out["samples"] - 1 >= 1
     assert out["socket_power_w_median"] in (1397, 1398, 1399)
