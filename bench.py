@@ -240,10 +240,8 @@ def workload_name(n: int, q: int, global_batch: int, world: int) -> str:
 
 def arith_name(q: int) -> str:
     """Kernel arithmetic class the library dispatches to for q (modarith.hpp)."""
-    if q < (1 << 30):
-        return "Arith32H"
     if q < (1 << 31):
-        return "Arith32P"  # Plantard twiddle products (arith_select.hpp default)
+        return "Arith32P"  # Plantard twiddle products (arith_select.hpp default, every q < 2^31)
     return "Arith32W" if q < (1 << 32) else "Arith64"
 
 

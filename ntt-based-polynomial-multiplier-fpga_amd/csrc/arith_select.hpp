@@ -4,9 +4,12 @@
 #pragma once
 #include <stdint.h>
 
-// Arith32H (Harvey bounds, Montgomery-form twiddles) for q < 2^30
+// Arith32H (Harvey bounds, Montgomery-form twiddles) for q < 2^30 (1); 0 = those q take Arith32P
+// as well (round 2: the Plantard kernels' bounds hold for every q < 2^31, and at q = 1073479681
+// they run n = 4096 products 9 % and n = 1024 products 7 % faster than Arith32H, kbench A/B
+// in profiles/r2/a32h_ab.txt)
 #ifndef NTTMUL_A32H
-#define NTTMUL_A32H 1
+#define NTTMUL_A32H 0
 #endif
 // Arith32P (Plantard twiddle products, canonical output for any 32-bit input) for the q < 2^31
 // not taken by Arith32H; 0 = the Montgomery Arith32 with typed butterflies (round-1 kernel)
@@ -64,12 +67,13 @@ constexpr bool p_signed_fw_entry(int logn, uint32_t idx) {
 // products of canonical values; the first four are folded by 2^32 mod q before the other four
 // are added.  With q = x 2^31 the sum is below x^2 (2 - x) 2^64 when 2^32 mod q = 2^32 - 2q
 // (x > 2/3) and below x^2 (2 - 1.5 x) 2^64 when it is 2^32 - 3q, so every 2^30 < q < 2^31
-// qualifies; the check is kept so a change of range cannot silently overflow
+// qualifies; below 2^30 the first four products stay under 2^62 and the fold under 2^62 + 2^32.
+// The check is kept so a change of range cannot silently overflow
 #ifndef NTTMUL_P3
 #define NTTMUL_P3 1
 #endif
 constexpr bool p3_fold_ok(uint64_t q) {
-  if (!NTTMUL_P3 || q >= (1ull << 31) || q < (1ull << 30)) return false;
+  if (!NTTMUL_P3 || q >= (1ull << 31) || q < 3) return false;
   const unsigned __int128 s1 = (unsigned __int128)4 * (q - 1) * (q - 1);  // < 2^64
   const unsigned __int128 c32 = ((unsigned __int128)1 << 32) % q;
   const unsigned __int128 fold = (s1 >> 32) * c32 + 0xFFFFFFFFu;
