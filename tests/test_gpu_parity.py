@@ -126,6 +126,60 @@ def test_random_vs_oracle(n, q, torch_cuda):
             assert np.array_equal(c[2], exp)
 
 
+def _random_primes(bits_list, step_log, seed):
+    """One random prime q = k 2^step_log + 1 of each bit length (oracle's Miller-Rabin)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for bits in bits_list:
+        bits = max(bits, step_log + 4)  # enough candidates k of that length
+        while True:
+            k = int(rng.integers(1 << (bits - step_log - 1), 1 << (bits - step_log)))
+            q = (k << step_log) + 1
+            if q.bit_length() == bits and O.is_prime(q):
+                out.append(q)
+                break
+    return out
+
+
+# every word/arithmetic class: Arith32P (incl. the D = 3 fold at n = 4096) below 2^31, Arith32W
+# in [2^31, 2^32), Arith64 above; the bit lengths straddle each class boundary
+_SWEEP_BITS = [14, 16, 20, 24, 28, 29, 30, 31, 31, 32, 32, 33, 36, 44, 52, 60, 61, 62, 62]
+
+
+@pytest.mark.parametrize("n", [256, 1024, 4096])
+def test_random_prime_sweep(n, torch_cuda):
+    """Random NTT-friendly primes of every bit length 14..62 (seeded, 2n | q - 1): a ragged
+    batch of random and extreme (all q - 1) operands, every product against the restated
+    reference product (NTT/ntt.C:342-371 / :428-451), in the native word and in 64-bit words."""
+    step = n.bit_length()  # 2n | q - 1
+    for q in _random_primes(_SWEEP_BITS, step, seed=n):
+        P = O.Plan(n, q)
+        ctx = _ctx(n, q)
+        a, b = O.fill_inputs(n, q, q & 0xFFFF, 5)
+        a[4] = q - 1
+        b[4] = q - 1
+        exp = np.stack([P.product_merged(a[i], b[i]) for i in range(5)])
+        dt = np.uint32 if q < (1 << 32) else np.uint64
+        c = ctx.multiply(a.astype(dt), b.astype(dt)).astype(np.uint64)
+        assert np.array_equal(c, exp), (n, q)
+        if dt == np.uint32:
+            assert np.array_equal(ctx.multiply(a, b, dtype=np.uint64), exp), (n, q, "u64 io")
+
+
+@pytest.mark.parametrize("n", [8192, 65536])
+def test_random_prime_sweep_multipass(n, torch_cuda):
+    """The multi-pass product over random primes of each word class (2^17 | q - 1)."""
+    for q in _random_primes([20, 30, 31, 32, 40, 62], 17, seed=n):
+        P = O.Plan(n, q)
+        ctx = _ctx(n, q)
+        a, b = O.fill_inputs(n, q, q & 0xFFFF, 2)
+        b[1] = q - 1
+        dt = np.uint32 if q < (1 << 32) else np.uint64
+        c = ctx.multiply(a.astype(dt), b.astype(dt)).astype(np.uint64)
+        for i in range(2):
+            assert np.array_equal(c[i], P.product_merged(a[i], b[i])), (n, q, i)
+
+
 @pytest.mark.parametrize("n", [8192, 16384, 32768, 65536])
 @pytest.mark.parametrize("q", [Q31, Q30, Q32, Q62, Q31HI, Q31LO])
 def test_multipass_vs_oracle(n, q, torch_cuda):
