@@ -214,6 +214,12 @@ __host__ __device__ constexpr bool kTypedP() {
 #ifndef NTTMUL_NT_MP
 #define NTTMUL_NT_MP 0
 #endif
+// column passes of the multi-pass product through non-temporal loads / stores: C5 1.375-1.383
+// vs 1.417-1.434 ms (kbench A/B, identical checksums, profiles/r2/nt_cols/); the row pass
+// keeps its intermediates temporal (NTTMUL_NT_MP = 1 measured 1.400 ms)
+#ifndef NTTMUL_NT_COLS
+#define NTTMUL_NT_COLS 1
+#endif
 template <bool NT, class T>
 __device__ __forceinline__ T ld_stream(const T *p) {
   if constexpr (NT) return __builtin_nontemporal_load(p);
@@ -677,8 +683,8 @@ __global__ __launch_bounds__(256) void k_cols_fwd(KParams<A> P, const TIn *__res
   W x[M], y[M];
 #pragma clang loop unroll(full)
   for (int m = 0; m < M; m++) {
-    x[m] = (W)a[base + ((size_t)m << logs)];
-    y[m] = NPOLY == 2 ? (W)b[base + ((size_t)m << logs)] : W(0);
+    x[m] = (W)ld_stream<NTTMUL_NT_COLS>(a + base + ((size_t)m << logs));
+    y[m] = NPOLY == 2 ? (W)ld_stream<NTTMUL_NT_COLS>(b + base + ((size_t)m << logs)) : W(0);
   }
 #pragma clang loop unroll(full)
   for (int st = 0; st < L1; st++) {
@@ -693,8 +699,8 @@ __global__ __launch_bounds__(256) void k_cols_fwd(KParams<A> P, const TIn *__res
   }
 #pragma clang loop unroll(full)
   for (int m = 0; m < M; m++) {
-    ta[base + ((size_t)m << logs)] = x[m];
-    if (NPOLY == 2) tb[base + ((size_t)m << logs)] = y[m];
+    st_stream<NTTMUL_NT_COLS>(ta + base + ((size_t)m << logs), x[m]);
+    if (NPOLY == 2) st_stream<NTTMUL_NT_COLS>(tb + base + ((size_t)m << logs), y[m]);
   }
 }
 
@@ -712,7 +718,7 @@ __global__ __launch_bounds__(256) void k_cols_inv(KParams<A> P,
   const size_t base = (p << (logs + L1)) + col;
   W x[M];
 #pragma clang loop unroll(full)
-  for (int m = 0; m < M; m++) x[m] = tc[base + ((size_t)m << logs)];
+  for (int m = 0; m < M; m++) x[m] = ld_stream<NTTMUL_NT_COLS>(tc + base + ((size_t)m << logs));
 #pragma clang loop unroll(full)
   for (int st = L1 - 1; st >= 0; st--) {
     const int dist = M >> (st + 1);
@@ -729,7 +735,8 @@ __global__ __launch_bounds__(256) void k_cols_inv(KParams<A> P,
   }
 #pragma clang loop unroll(full)
   for (int m = 0; m < M; m++)
-    c[base + ((size_t)m << logs)] = (TOut)(A::kInvCanonical ? x[m] : P.ar.canon(x[m]));
+    st_stream<NTTMUL_NT_COLS>(c + base + ((size_t)m << logs),
+                              (TOut)(A::kInvCanonical ? x[m] : P.ar.canon(x[m])));
 }
 
 // ---------------------------------------------------------------------------------------------
