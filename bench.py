@@ -69,8 +69,9 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--n", type=int, default=4096)
     ap.add_argument("--q", type=int, default=2013265921)
-    ap.add_argument("--batch-per-gpu", type=int, default=0,
-                    help="0: 65536 (C3) per GPU, or 2^20 / 8 at 8 ranks (C4: batch 2^20 over 8 GPUs)")
+    ap.add_argument("--batch-per-gpu", type=int, default=65536,
+                    help="polymults per GPU per step, the same at every N (weak scaling; default "
+                         "C3's 65536; C4 = --batch-per-gpu 131072 at 8 ranks: 2^20 in all)")
     ap.add_argument("--word-bits", type=int, default=0, help="32/64 coefficient storage (0: auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-io", action="store_true",
@@ -103,7 +104,8 @@ def cpu_baseline(n: int, q: int, target_s: float):
     import numpy as np
     from oracle import oracle as O
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or O.num_threads()
+    cores = host_cores()
+    threads = cores["threads"]
     P = O.Plan(n, q)
     if q >= (1 << 31):
         return None
@@ -126,6 +128,7 @@ def cpu_baseline(n: int, q: int, target_s: float):
         variants[name] = {"value": per * r / tt, "unit": "polymults/s",
                           "us_per_polymult_per_core": tt / (per * r) * threads * 1e6}
     anchors = {k: {"us_per_polymult": v * 1e6, "cores": 1} for k, v in O.ref_anchors().items()}
+    c1 = c1_single(target_s=min(2.0, 0.2 * target_s))
     model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -137,10 +140,56 @@ def cpu_baseline(n: int, q: int, target_s: float):
     return {"value": value, "unit": "polymults/s", "cores": threads, "kind": "port",
             "us_per_polymult_per_core": threads / value * 1e6,
             "sample": f"{per * reps} polymults (n={n}, q={q}) = {reps} passes over {per} "
-                      f"counter-based inputs, OpenMP {threads} threads of {os.cpu_count()} "
-                      f"({model}), {total_t:.1f} s, oracle/nttmul_oracle.c orc_fast_batch_u32",
+                      f"counter-based inputs, OpenMP {threads} threads ({model}), "
+                      f"{total_t:.1f} s, oracle/nttmul_oracle.c orc_fast_batch_u32",
+            "host_cores": cores,
+            "c1": c1,
             "variants": variants,
             "reference_anchors": anchors or "oracle/_ref not built (no reference tree)"}
+
+
+def host_cores() -> dict:
+    """The host cores this process may use, and the OpenMP thread count the CPU baseline takes:
+    every core of the affinity mask, capped by the cgroup CPU quota and by OMP_NUM_THREADS when
+    either is set (the GPU box exports OMP_NUM_THREADS = its per-GPU CPU share)."""
+    total = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = total
+    quota = None
+    try:  # cgroup v2: "<quota> <period>" or "max <period>"
+        qs, ps = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if qs != "max":
+            quota = max(1, int(int(qs) / int(ps)))
+    except (OSError, ValueError):
+        pass
+    omp_env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or None
+    threads = min(x for x in (affinity, quota, omp_env) if x)
+    limits = [k for k, v in (("affinity", affinity), ("cgroup cpu.max", quota),
+                             ("OMP_NUM_THREADS", omp_env)) if v == threads]
+    return {"threads": threads, "os_cpu_count": total, "sched_getaffinity": affinity,
+            "cgroup_cpu_quota": quota, "OMP_NUM_THREADS": omp_env,
+            "rule": f"min(affinity, cgroup quota, OMP_NUM_THREADS) = {threads} "
+                    f"(set by {', '.join(limits)})"}
+
+
+def c1_single(n: int = 1024, q: int = 2013265921, target_s: float = 2.0):
+    """BASELINE.json configs[0] (C1): the unoptimized Cooley-Tukey product (ntt256.C:5-13
+    sequence, restated at this (n, q)) on ONE host core, ONE polymult per call, timed as
+    time_testing256.c:147-187 (inputs restored untimed, CLOCK_MONOTONIC around each call,
+    averaged); checked against the oracle's merged product before it is reported."""
+    from oracle import oracle as O
+    P = O.Plan(n, q)
+    a, b = O.fill_inputs(n, q, 0, 1)
+    c, t = P.time_single(a[0], b[0], gs=False, reps=30)      # time_testing256.c: 30 calls
+    reps = max(30, int(target_s / max(t, 1e-9)))
+    c, t = P.time_single(a[0], b[0], gs=False, reps=reps)
+    ok = bool((c == P.product_merged(a[0], b[0])).all())
+    return {"value": 1.0 / t, "unit": "polymults/s", "us_per_polymult": t * 1e6, "cores": 1,
+            "n": n, "q": q, "kind": "port", "matches_oracle": ok,
+            "sample": f"{reps} single products (counter-based input 0), ntt256.C:5-13 CT sequence "
+                      "(oracle/nttmul_oracle.c orc_time_single), one thread"}
 
 
 def host_io(ctx, a_dev, b_dev, batch: int, n: int, wb: int, reps: int = 3):
@@ -236,13 +285,6 @@ def workload_name(n: int, q: int, global_batch: int, world: int) -> str:
     if n == 65536 and q >= (1 << 32) and global_batch == 1024 * world:
         return "C5"
     return "custom"
-
-
-def arith_name(q: int) -> str:
-    """Kernel arithmetic class the library dispatches to for q (modarith.hpp)."""
-    if q < (1 << 31):
-        return "Arith32P"  # Plantard twiddle products (arith_select.hpp default, every q < 2^31)
-    return "Arith32W" if q < (1 << 32) else "Arith64"
 
 
 IC_BYTES = 256 << 20        # MI355X Infinity Cache (MI355X_MICROARCH.md)
@@ -397,8 +439,8 @@ def main(argv=None):
 
     n, q = args.n, args.q
     wb = args.word_bits or (32 if q < (1 << 32) else 64)
-    # weak scaling: C3's 65536 polymults per GPU; at 8 ranks the global batch is C4's 2^20
-    batch = args.batch_per_gpu or ((1 << 20) // world if world == 8 else 65536)
+    # weak scaling: the same --batch-per-gpu at every N (C3's 65536 by default)
+    batch = args.batch_per_gpu
     global_batch = batch * world
     p0, p1 = shard(global_batch, rank, world)
     count = p1 - p0
@@ -406,8 +448,8 @@ def main(argv=None):
     alg_bytes = 3 * n * wbytes * count                    # read a, b + write c, per launch
     rotate = buffer_sets(alg_bytes, args.rotate)
     nstreams = max(1, args.streams)
-    if nstreams > 1:  # concurrent steps never share an output buffer
-        rotate = max(rotate, nstreams)
+    if nstreams > 1:  # each buffer set always goes to the same stream (no cross-stream reuse)
+        rotate = -(-max(rotate, nstreams) // nstreams) * nstreams
 
     ctx = nttmul.Context(n, q, ndev=1, first_dev=devno)
     dt = torch.int32 if wb == 32 else torch.int64
@@ -489,9 +531,7 @@ def main(argv=None):
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": traffic_source,
-                         "kernel": (f"k_rows<{arith_name(q)},u32,u32,{n.bit_length() - 1},0>"
-                                    if (single_launch and wb == 32)
-                                    else "polymul (all launches of one step)"),
+                         "kernel": ctx.kernel_name(wb),
                          "kernel_ms": kern_ms,
                          "alg_bytes_per_launch": alg_bytes,
                          "buffer_sets": rotate,

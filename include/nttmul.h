@@ -48,6 +48,9 @@ extern "C" {
 #define NTTMUL_FLAG_VALIDATE 1u  /* range-check inputs on the device before multiplying */
 #define NTTMUL_FLAG_CYCLIC 2u    /* FPGA-compat: c = a*b mod (x^n - 1, q) (Hardware_Multiplier/
                                     PolyMult.v); q == 1 (mod n); params.psi carries omega */
+#define NTTMUL_FLAG_SHARE_DEVICES 4u /* params.ndev slices may exceed the visible devices: slice i
+                                    runs on device first_dev + i mod (count - first_dev), with its
+                                    own streams and buffers (the multi-device split on one GPU) */
 
 typedef struct nttmul_ctx nttmul_ctx;
 
@@ -55,7 +58,8 @@ typedef struct {
   uint32_t n;          /* ring degree, power of two, 256 <= n <= 65536                          */
   uint64_t q;          /* prime, q == 1 (mod 2n), q < 2^62                                       */
   uint64_t psi;        /* primitive 2n-th root of unity; 0 = smallest one (generate_params.C:25) */
-  int ndev;            /* devices to split host-buffer batches over; <= 0 = all visible devices  */
+  int ndev;            /* devices (slices) to split host-buffer batches over, each driven by its
+                          own host thread; <= 0 = all visible devices                           */
   int first_dev;       /* first HIP device index used                                           */
   uint32_t flags;      /* NTTMUL_FLAG_*                                                          */
 } nttmul_params;
@@ -79,6 +83,15 @@ const char *nttmul_strerror(int status);
 /* last HIP error string recorded on ctx ("" if none) */
 const char *nttmul_last_error(const nttmul_ctx *ctx);
 int nttmul_get_info(const nttmul_ctx *ctx, nttmul_info *info);
+/* Diagnostics (no reference counterpart): the device kernel(s) one product call with word_bits
+ * storage dispatches to, as rocprofv3 names them with template arguments, e.g.
+ * "k_rows<Arith32P3,u32,u32,12,0>" (n > 4096: the passes joined by " + ").  Copies at most
+ * cap - 1 characters and a NUL into buf; returns the full length, or a negative status. */
+int nttmul_kernel_name(const nttmul_ctx *ctx, int word_bits, char *buf, size_t cap);
+/* Diagnostics: how the last host-buffer call on ctx moved its first chunk: 0 staged through
+ * pinned buffers, 1 direct DMA from / to page-locked caller memory, 2 zero-copy kernel access to
+ * the pinned staging buffers; -1 before any call. */
+int nttmul_last_host_path(const nttmul_ctx *ctx);
 
 /* multiply(a, b, n, q) -> c for one polynomial; host buffers of n words.
  * ≙ mode-1 + mode-2 + mode-3 + FIFO read of NTT_HARDWARE_EXE (NTT_PCIECommunicationv2.c:183-224) */

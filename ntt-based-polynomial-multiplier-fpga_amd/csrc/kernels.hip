@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
 #include <type_traits>
 
 #include "launch.hpp"
@@ -89,6 +90,13 @@
 #ifndef NTTMUL_ABL_NOSTORE
 #define NTTMUL_ABL_NOSTORE 0
 #endif
+// The ablation switches above give wrong products by design: they compile only into the
+// tools/kbench timing binaries (tools/kbench/build.sh passes NTTMUL_KBENCH_BUILD), never into
+// libnttmul.so
+#if (NTTMUL_ABL_TWMASK || NTTMUL_ABL_NOLOAD || NTTMUL_ABL_NOXCHG || NTTMUL_ABL_NOSTORE || \
+     NTTMUL_KBENCH_LITE || defined(NTTMUL_ABL_L2LOAD)) && !defined(NTTMUL_KBENCH_BUILD)
+#error "NTTMUL_ABL_* / NTTMUL_KBENCH_LITE are wrong-result kbench switches (tools/kbench/build.sh only)"
+#endif
 
 namespace nttmul {
 
@@ -103,6 +111,17 @@ struct KParams {
   typename A::word f, fs;              // F  = n^-1 R mod q (R = Montgomery radix)
   typename A::word wf, wfs;            // iw[1] * F mod q
 };
+
+// Dry run of the product dispatch (describe_polymul -> nttmul_kernel_name): while tl_describe is
+// set, the launchers append the kernels they would launch to it and launch nothing, so the name
+// the bench reports comes from the same dispatch code that runs.
+static thread_local std::string *tl_describe = nullptr;
+template <class A> struct AName;
+template <class T> constexpr const char *word_name() { return sizeof(T) == 8 ? "u64" : "u32"; }
+static void describe_add(const std::string &k) {
+  if (!tl_describe->empty()) *tl_describe += " + ";
+  *tl_describe += k;
+}
 
 // ---------------------------------------------------------------------------------------------
 // Layout algebra of the register groups (all compile-time except the per-thread base)
@@ -201,6 +220,12 @@ template <>
 struct IsPlantard<Arith32P> : std::true_type {};
 template <>
 struct IsPlantard<Arith32P3> : std::true_type {};
+template <> struct AName<Arith32> { static constexpr const char *v = "Arith32"; };
+template <> struct AName<Arith32H> { static constexpr const char *v = "Arith32H"; };
+template <> struct AName<Arith32P> { static constexpr const char *v = "Arith32P"; };
+template <> struct AName<Arith32P3> { static constexpr const char *v = "Arith32P3"; };
+template <> struct AName<Arith32W> { static constexpr const char *v = "Arith32W"; };
+template <> struct AName<Arith64> { static constexpr const char *v = "Arith64"; };
 template <class A>
 __host__ __device__ constexpr bool kTypedP() {
   if constexpr (IsPlantard<A>::value) return A::kTypedP;
@@ -831,6 +856,11 @@ static hipError_t launch_rows(const KParams<A> &P, const void *a, const void *b,
                               size_t units, hipStream_t s) {
   constexpr int NT = rows_threads(LOGS), PB = NT / ((1 << LOGS) / 16);
   const size_t blocks = (units + PB - 1) / PB;
+  if (tl_describe) {
+    describe_add(std::string("k_rows<") + AName<A>::v + "," + word_name<TIn>() + "," +
+                 word_name<TOut>() + "," + std::to_string(LOGS) + "," + std::to_string(L1) + ">");
+    return hipSuccess;
+  }
   if (blocks == 0) return hipSuccess;
   hipLaunchKernelGGL((k_rows<A, TIn, TOut, LOGS, L1>), dim3((unsigned)blocks), dim3(NT), 0, s, P,
                      (const TIn *)a, (const TIn *)b, (TOut *)c, units);
@@ -860,6 +890,14 @@ static hipError_t multipass_l1(const LaunchTables &T, const void *a, const void 
   const KParams<A> P = product_params<A>(T);
   const size_t cols = batch << LOGS;
   const unsigned cblocks = (unsigned)((cols + 255) / 256);
+  if (tl_describe) {
+    const std::string args = std::string(AName<A>::v) + "," + word_name<IO>() + "," +
+                             std::to_string(L1);
+    describe_add("k_cols_fwd<" + args + ">");
+    (void)launch_rows<A, W, W, LOGS, L1>(P, ta, tb, tc, batch << L1, s);
+    describe_add("k_cols_inv<" + args + ">");
+    return hipSuccess;
+  }
   hipLaunchKernelGGL((k_cols_fwd<A, IO, L1>), dim3(cblocks), dim3(256), 0, s, P, (const IO *)a,
                      (const IO *)b, (W *)ta, (W *)tb, batch, LOGS);
   hipError_t e = hipGetLastError();
@@ -931,6 +969,15 @@ hipError_t launch_polymul(const LaunchTables &T, const void *a, const void *b, v
   }
   return polymul_io<Arith64>(T, a, b, c, batch, io_bits, scr, s);
 #endif
+}
+
+hipError_t describe_polymul(const LaunchTables &T, int io_bits, std::string *out) {
+  out->clear();
+  void *scr[3] = {nullptr, nullptr, nullptr};
+  tl_describe = out;
+  const hipError_t e = launch_polymul(T, nullptr, nullptr, nullptr, 1, io_bits, scr, nullptr);
+  tl_describe = nullptr;
+  return e;
 }
 
 template <class A, class TIn, class TOut, int LOGS, int L1, int DIR>

@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <condition_variable>
 #include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -85,6 +86,7 @@ struct nttmul_ctx {
   int ndev = 0;
   DevState dev[kMaxDev];
   char err[256] = {0};
+  int last_path = -1;                         // run_host: 0 staged, 1 direct DMA, 2 zero-copy
 };
 
 namespace {
@@ -98,8 +100,14 @@ struct DeviceGuard {
   }
 };
 
+// (the host-buffer path drives several devices from their own threads: one writer at a time)
+std::mutex g_err_mu;
+
 int fail(nttmul_ctx *ctx, hipError_t e, const char *what) {
-  if (ctx) snprintf(ctx->err, sizeof(ctx->err), "%s: %s", what, hipGetErrorString(e));
+  if (ctx) {
+    std::lock_guard<std::mutex> l(g_err_mu);
+    snprintf(ctx->err, sizeof(ctx->err), "%s: %s", what, hipGetErrorString(e));
+  }
   return e == hipErrorOutOfMemory ? NTTMUL_ENOMEM : NTTMUL_EHIP;
 }
 
@@ -409,25 +417,118 @@ int ensure_slots(nttmul_ctx *ctx, DevState &d, size_t bytes) {
   return NTTMUL_OK;
 }
 
-// True when [p, p + bytes) lies in page-locked host memory the copy engines can DMA directly
-// (hipHostMalloc'd or hipHostRegister'ed; both ends checked, the range may span two such blocks).
+// True when [p, p + bytes) lies inside ONE page-locked host allocation the copy engines can DMA
+// directly (hipHostMalloc'd or hipHostRegister'ed): the allocation that holds p (its device
+// view's address range) must also hold p + bytes - 1.  Anything else — pageable memory, a range
+// spanning two pinned blocks or pageable memory between two pinned ends — takes the staged path.
 bool host_pinned(const void *p, size_t bytes) {
   if (!p || !bytes) return false;
-  for (const void *q : {p, (const void *)((const char *)p + bytes - 1)}) {
-    hipPointerAttribute_t at;
-    if (hipPointerGetAttributes(&at, q) != hipSuccess) {
-      (void)hipGetLastError();  // pageable memory: the query fails, clear the sticky error
-      return false;
-    }
-    if (at.type != hipMemoryTypeHost) return false;
+  hipPointerAttribute_t at;
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();  // pageable memory: the query fails, clear the sticky error
+    return false;
   }
-  return true;
+  if (at.type != hipMemoryTypeHost || !at.devicePointer) return false;
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)at.devicePointer) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  const char *d0 = (const char *)at.devicePointer, *b0 = (const char *)base;
+  return d0 >= b0 && (size_t)(d0 - b0) <= size && bytes <= size - (size_t)(d0 - b0);
 }
 
 // Host-buffer path (the FPGA transaction: mode 1/2 DMA in, mode 3, DMA out).  Each device's
-// contiguous slice streams through kSlots pipeline slots in chunks: the host copies
-// chunk j into pinned staging while the GPU runs H2D -> kernel -> D2H of chunks j-1, j-2 on the
-// other slots' streams, and copies a finished chunk's result out when its slot comes round again.
+// contiguous slice [p0, p1) streams through kSlots pipeline slots in chunks: the host
+// copies chunk j into pinned staging while the GPU runs H2D -> kernel -> D2H of chunks j-1, j-2 on
+// the other slots' streams, and copies a finished chunk's result out when its slot comes round
+// again.  `direct`: a, b, c are page-locked, so the copy engines DMA each chunk straight from and
+// to them and the host only waits at the end.
+struct HostJob {
+  int op, io_bits;
+  void *c;
+  const void *a, *b;
+  size_t pbytes, chunk, zero_copy;
+  bool direct;
+};
+
+int run_host_dev(nttmul_ctx *ctx, DevState &d, const HostJob &J, size_t p0, size_t p1) {
+  const bool two = J.op == OP_MULTIPLY || J.op == OP_POINTWISE;
+  struct Pending {
+    bool busy = false;
+    size_t off = 0, bytes = 0;
+  } slot[kSlots];
+  HIP_TRY(ctx, hipSetDevice(d.id));
+  int st = ensure_slots(ctx, d, std::min(J.chunk, p1 - p0) * J.pbytes);
+  if (st) return st;
+  auto retire = [&](int s) -> int {
+    Pending &pd = slot[s];
+    if (!pd.busy) return NTTMUL_OK;
+    pd.busy = false;
+    HIP_TRY(ctx, hipStreamSynchronize(d.xs[s]));
+    if (!J.direct) pcopy((char *)J.c + pd.off, d.pin[s][2], pd.bytes);
+    return NTTMUL_OK;
+  };
+  unsigned k = 0;
+  for (size_t next = p0; next < p1 && !st;) {
+    const int s = (int)(k++ % kSlots);
+    const size_t cnt = std::min(J.chunk, p1 - next);
+    const size_t off = next * J.pbytes, bytes = cnt * J.pbytes;
+    hipError_t e = hipSuccess;
+    if (J.direct) {
+      e = hipMemcpyAsync(d.dbuf[s][0], (const char *)J.a + off, bytes, hipMemcpyHostToDevice,
+                         d.xs[s]);
+      if (e == hipSuccess && two)
+        e = hipMemcpyAsync(d.dbuf[s][1], (const char *)J.b + off, bytes, hipMemcpyHostToDevice,
+                           d.xs[s]);
+      if (e != hipSuccess) { st = fail(ctx, e, "hipMemcpyAsync H2D"); break; }
+      if ((st = run_device(ctx, d, d.sscr[s], J.op, d.dbuf[s][2], d.dbuf[s][0], d.dbuf[s][1],
+                           cnt, J.io_bits, d.xs[s])))
+        break;
+      e = hipMemcpyAsync((char *)J.c + off, d.dbuf[s][2], bytes, hipMemcpyDeviceToHost, d.xs[s]);
+      if (e != hipSuccess) { st = fail(ctx, e, "hipMemcpyAsync D2H"); break; }
+      slot[s] = Pending{true, off, bytes};
+      next += cnt;
+      continue;
+    }
+    if ((st = retire(s))) break;
+    pcopy(d.pin[s][0], (const char *)J.a + off, bytes);
+    if (two) pcopy(d.pin[s][1], (const char *)J.b + off, bytes);
+    if (bytes <= J.zero_copy && ctx->plan.logn <= 12) {
+      // small transaction (the ntt256_product* shims): the kernel reads a, b from and writes c to
+      // the pinned staging buffers over PCIe — no copy-engine round trips
+      if ((st = run_device(ctx, d, d.sscr[s], J.op, d.pin_dev[s][2], d.pin_dev[s][0],
+                           d.pin_dev[s][1], cnt, J.io_bits, d.xs[s])))
+        break;
+      slot[s] = Pending{true, off, bytes};
+      next += cnt;
+      continue;
+    }
+    e = hipMemcpyAsync(d.dbuf[s][0], d.pin[s][0], bytes, hipMemcpyHostToDevice, d.xs[s]);
+    if (e == hipSuccess && two)
+      e = hipMemcpyAsync(d.dbuf[s][1], d.pin[s][1], bytes, hipMemcpyHostToDevice, d.xs[s]);
+    if (e != hipSuccess) { st = fail(ctx, e, "hipMemcpyAsync H2D"); break; }
+    if ((st = run_device(ctx, d, d.sscr[s], J.op, d.dbuf[s][2], d.dbuf[s][0], d.dbuf[s][1], cnt,
+                         J.io_bits, d.xs[s])))
+      break;
+    e = hipMemcpyAsync(d.pin[s][2], d.dbuf[s][2], bytes, hipMemcpyDeviceToHost, d.xs[s]);
+    if (e != hipSuccess) { st = fail(ctx, e, "hipMemcpyAsync D2H"); break; }
+    slot[s] = Pending{true, off, bytes};
+    next += cnt;
+  }
+  // drain (also after an error, so no slot is left in flight and no DMA still touches the
+  // caller's buffers when the call returns)
+  for (int s = 0; s < kSlots; s++) {
+    const int r = retire(s);
+    if (!st) st = r;
+  }
+  return st;
+}
+
+// The batch splits into one contiguous slice per context device; with several devices each slice
+// is driven by its own host thread (slice 0 by the caller's), so one device's staging copies and
+// synchronisations never stall another's pipeline.
 int run_host(nttmul_ctx *ctx, int op, void *c, const void *a, const void *b, size_t batch,
              int io_bits) {
   const bool two = op == OP_MULTIPLY || op == OP_POINTWISE;
@@ -435,121 +536,38 @@ int run_host(nttmul_ctx *ctx, int op, void *c, const void *a, const void *b, siz
   if (io_bits != 32 && io_bits != 64) return NTTMUL_EINVAL;
   if (!batch) return NTTMUL_OK;
   DeviceGuard guard;
-  const size_t pbytes = (size_t)ctx->plan.n * (io_bits / 8);
-  const size_t chunk = std::max<size_t>(1, kChunkBytes / pbytes);
+  HostJob J;
+  J.op = op;
+  J.io_bits = io_bits;
+  J.c = c;
+  J.a = a;
+  J.b = b;
+  J.pbytes = (size_t)ctx->plan.n * (io_bits / 8);
+  J.chunk = std::max<size_t>(1, kChunkBytes / J.pbytes);
   // per-operand bytes up to which a chunk runs zero-copy on the pinned staging buffers
   // (NTTMUL_ZEROCOPY_KB, default 64; 0 never)
   const char *zc_env = getenv("NTTMUL_ZEROCOPY_KB");
-  const size_t zero_copy = (zc_env ? (size_t)atol(zc_env) : 64) << 10;
-  struct Pending {
-    bool busy = false;
-    size_t off = 0, bytes = 0;
-  };
-  struct Job {
-    size_t next = 0, end = 0;
-    unsigned k = 0;
-    Pending slot[kSlots];
-  } job[kMaxDev];
-  size_t p0 = 0;
-  for (int i = 0; i < ctx->ndev; i++) {
-    const size_t p1 = batch * (size_t)(i + 1) / ctx->ndev;
-    job[i].next = p0;
-    job[i].end = p1;
-    if (p1 > p0) {
-      HIP_TRY(ctx, hipSetDevice(ctx->dev[i].id));
-      int st = ensure_slots(ctx, ctx->dev[i], std::min(chunk, p1 - p0) * pbytes);
-      if (st) return st;
-    }
-    p0 = p1;
+  J.zero_copy = (zc_env ? (size_t)atol(zc_env) : 64) << 10;
+  const size_t total = batch * J.pbytes;
+  J.direct = host_pinned(a, total) && (!two || host_pinned(b, total)) && host_pinned(c, total);
+  const size_t first_chunk = std::min(J.chunk, std::max<size_t>(1, batch / ctx->ndev));
+  ctx->last_path = J.direct ? 1 : (first_chunk * J.pbytes <= J.zero_copy &&
+                                   ctx->plan.logn <= 12) ? 2 : 0;
+  int status[kMaxDev] = {};
+  std::vector<std::thread> th;
+  for (int i = 1; i < ctx->ndev; i++) {
+    const size_t p0 = batch * (size_t)i / ctx->ndev, p1 = batch * (size_t)(i + 1) / ctx->ndev;
+    if (p1 > p0)
+      th.emplace_back([ctx, &J, &status, i, p0, p1] {
+        status[i] = run_host_dev(ctx, ctx->dev[i], J, p0, p1);
+      });
   }
-  // page-locked caller buffers: DMA straight from / to them, no staging copies (retire only
-  // waits, and only at the end: a slot's stream orders its own chunks)
-  const size_t total = batch * pbytes;
-  const bool direct = host_pinned(a, total) && (!two || host_pinned(b, total)) &&
-                      host_pinned(c, total);
-  auto retire = [&](int i, int s) -> int {
-    DevState &d = ctx->dev[i];
-    Pending &pd = job[i].slot[s];
-    if (!pd.busy) return NTTMUL_OK;
-    HIP_TRY(ctx, hipSetDevice(d.id));
-    HIP_TRY(ctx, hipStreamSynchronize(d.xs[s]));
-    if (!direct) pcopy((char *)c + pd.off, d.pin[s][2], pd.bytes);
-    pd.busy = false;
-    return NTTMUL_OK;
-  };
-  int st = NTTMUL_OK;
-  for (bool more = true; more && !st;) {
-    more = false;
-    for (int i = 0; i < ctx->ndev && !st; i++) {
-      Job &J = job[i];
-      if (J.next >= J.end) continue;
-      more = true;
-      DevState &d = ctx->dev[i];
-      const int s = (int)(J.k++ % kSlots);
-      const size_t cnt = std::min(chunk, J.end - J.next);
-      const size_t off = J.next * pbytes, bytes = cnt * pbytes;
-      if (direct) {
-        HIP_TRY(ctx, hipSetDevice(d.id));
-        hipError_t e = hipMemcpyAsync(d.dbuf[s][0], (const char *)a + off, bytes,
-                                      hipMemcpyHostToDevice, d.xs[s]);
-        if (e == hipSuccess && two)
-          e = hipMemcpyAsync(d.dbuf[s][1], (const char *)b + off, bytes, hipMemcpyHostToDevice,
-                             d.xs[s]);
-        if (e != hipSuccess) {
-          st = fail(ctx, e, "hipMemcpyAsync H2D");
-          break;
-        }
-        if ((st = run_device(ctx, d, d.sscr[s], op, d.dbuf[s][2], d.dbuf[s][0], d.dbuf[s][1],
-                             cnt, io_bits, d.xs[s])))
-          break;
-        e = hipMemcpyAsync((char *)c + off, d.dbuf[s][2], bytes, hipMemcpyDeviceToHost, d.xs[s]);
-        if (e != hipSuccess) {
-          st = fail(ctx, e, "hipMemcpyAsync D2H");
-          break;
-        }
-        J.slot[s] = Pending{true, off, bytes};
-        J.next += cnt;
-        continue;
-      }
-      if ((st = retire(i, s))) break;
-      pcopy(d.pin[s][0], (const char *)a + off, bytes);
-      if (two) pcopy(d.pin[s][1], (const char *)b + off, bytes);
-      if (bytes <= zero_copy && ctx->plan.logn <= 12) {
-        // small transaction (the ntt256_product* shims): the kernel reads a, b from and writes
-        // c to the pinned staging buffers over PCIe — no copy-engine round trips
-        if ((st = run_device(ctx, d, d.sscr[s], op, d.pin_dev[s][2], d.pin_dev[s][0],
-                             d.pin_dev[s][1], cnt, io_bits, d.xs[s])))
-          break;
-        J.slot[s] = Pending{true, off, bytes};
-        J.next += cnt;
-        continue;
-      }
-      hipError_t e = hipMemcpyAsync(d.dbuf[s][0], d.pin[s][0], bytes, hipMemcpyHostToDevice, d.xs[s]);
-      if (e == hipSuccess && two)
-        e = hipMemcpyAsync(d.dbuf[s][1], d.pin[s][1], bytes, hipMemcpyHostToDevice, d.xs[s]);
-      if (e != hipSuccess) {
-        st = fail(ctx, e, "hipMemcpyAsync H2D");
-        break;
-      }
-      if ((st = run_device(ctx, d, d.sscr[s], op, d.dbuf[s][2], d.dbuf[s][0], d.dbuf[s][1], cnt,
-                           io_bits, d.xs[s])))
-        break;
-      e = hipMemcpyAsync(d.pin[s][2], d.dbuf[s][2], bytes, hipMemcpyDeviceToHost, d.xs[s]);
-      if (e != hipSuccess) {
-        st = fail(ctx, e, "hipMemcpyAsync D2H");
-        break;
-      }
-      J.slot[s] = Pending{true, off, bytes};
-      J.next += cnt;
-    }
-  }
-  // drain (also after an error, so no slot is left in flight)
+  const size_t p1 = batch / ctx->ndev;
+  if (p1 > 0) status[0] = run_host_dev(ctx, ctx->dev[0], J, 0, p1);
+  for (std::thread &t : th) t.join();
   for (int i = 0; i < ctx->ndev; i++)
-    for (int s = 0; s < kSlots; s++) {
-      int r = retire(i, s);
-      if (!st) st = r;
-    }
-  return st;
+    if (status[i]) return status[i];
+  return NTTMUL_OK;
 }
 
 }  // namespace
@@ -609,7 +627,10 @@ int nttmul_create_ex(nttmul_ctx **out, const nttmul_params *prm) {
   }
   const int first = prm->first_dev < 0 ? 0 : prm->first_dev;
   int ndev = prm->ndev <= 0 ? count - first : prm->ndev;
-  if (first >= count || ndev <= 0 || first + ndev > count || ndev > kMaxDev) {
+  // NTTMUL_FLAG_SHARE_DEVICES: ndev slices over the devices first .. count - 1 round-robin (as
+  // bench.py maps ranks), so the multi-device split also runs on a single GPU
+  const bool share = (prm->flags & NTTMUL_FLAG_SHARE_DEVICES) != 0;
+  if (first >= count || ndev <= 0 || (!share && first + ndev > count) || ndev > kMaxDev) {
     delete ctx;
     return NTTMUL_ENODEV;
   }
@@ -617,7 +638,7 @@ int nttmul_create_ex(nttmul_ctx **out, const nttmul_params *prm) {
   const size_t tbytes = ctx->plan.fw.size();
   for (int i = 0; i < ndev; i++) {
     DevState &d = ctx->dev[i];
-    d.id = first + i;
+    d.id = first + i % (count - first);
     ctx->ndev = i + 1;
     hipError_t e;
     if ((e = hipSetDevice(d.id)) != hipSuccess ||
@@ -693,6 +714,22 @@ int nttmul_get_info(const nttmul_ctx *ctx, nttmul_info *info) {
   info->kernel = P.logn > 12 ? 2 : 1;
   info->cyclic = P.cyclic ? 1 : 0;
   return NTTMUL_OK;
+}
+
+int nttmul_last_host_path(const nttmul_ctx *ctx) { return ctx ? ctx->last_path : NTTMUL_EINVAL; }
+
+int nttmul_kernel_name(const nttmul_ctx *ctx, int word_bits, char *buf, size_t cap) {
+  if (!ctx || (word_bits != 32 && word_bits != 64) || (cap && !buf)) return NTTMUL_EINVAL;
+  if (word_bits == 32 && ctx->plan.q > 0xFFFFFFFFull) return NTTMUL_EINVAL;
+  std::string name;
+  if (describe_polymul(tables_for(ctx, ctx->dev[0]), word_bits, &name) != hipSuccess)
+    return NTTMUL_EUNSUPPORTED;
+  if (cap) {
+    const size_t k = std::min(cap - 1, name.size());
+    memcpy(buf, name.data(), k);
+    buf[k] = 0;
+  }
+  return (int)name.size();
 }
 
 int nttmul_multiply_batch_u32(nttmul_ctx *ctx, uint32_t *c, const uint32_t *a, const uint32_t *b,

@@ -28,6 +28,7 @@ NTTMUL_ERANGE = -5
 NTTMUL_EUNSUPPORTED = -6
 NTTMUL_FLAG_VALIDATE = 1
 NTTMUL_FLAG_CYCLIC = 2
+NTTMUL_FLAG_SHARE_DEVICES = 4
 # transform modes (include/nttmul.h nttmul_transform_*)
 XF_FORWARD = 0
 XF_INVERSE = 1
@@ -89,6 +90,8 @@ def load_library() -> ctypes.CDLL:
     lib.nttmul_last_error.argtypes = [vp]
     lib.nttmul_last_error.restype = ctypes.c_char_p
     lib.nttmul_get_info.argtypes = [vp, ctypes.POINTER(Info)]
+    lib.nttmul_kernel_name.argtypes = [vp, i32, ctypes.c_char_p, sz]
+    lib.nttmul_last_host_path.argtypes = [vp]
     for name in ("nttmul_multiply_u32", "nttmul_multiply_u64"):
         getattr(lib, name).argtypes = [vp, vp, vp, vp]
     for name in ("nttmul_multiply_batch_u32", "nttmul_multiply_batch_u64"):
@@ -202,12 +205,14 @@ class Context:
     """An (n, q) multiplier bound to one or more HIP devices (≙ an opened FPGA handle)."""
 
     def __init__(self, n: int, q: int, psi: int = 0, ndev: int = 1, first_dev: int = 0,
-                 validate: bool = False, cyclic: bool = False):
+                 validate: bool = False, cyclic: bool = False, share_devices: bool = False):
         """cyclic=True: FPGA-compat product mod (x^n - 1, q) (Hardware_Multiplier/PolyMult.v);
-        `psi` then carries the primitive n-th root omega (0 = the smallest one)."""
+        `psi` then carries the primitive n-th root omega (0 = the smallest one).
+        share_devices=True: `ndev` slices may map several onto one device (round-robin)."""
         self._lib = load_library()
         self._h = ctypes.c_void_p()
-        flags = (NTTMUL_FLAG_VALIDATE if validate else 0) | (NTTMUL_FLAG_CYCLIC if cyclic else 0)
+        flags = ((NTTMUL_FLAG_VALIDATE if validate else 0) | (NTTMUL_FLAG_CYCLIC if cyclic else 0)
+                 | (NTTMUL_FLAG_SHARE_DEVICES if share_devices else 0))
         prm = _Params(n, q, psi, ndev, first_dev, flags)
         st = self._lib.nttmul_create_ex(ctypes.byref(self._h), ctypes.byref(prm))
         if st != NTTMUL_OK:
@@ -239,6 +244,20 @@ class Context:
     def _check(self, st: int):
         if st != NTTMUL_OK:
             raise NttmulError(st, f"{strerror(st)}: {self._lib.nttmul_last_error(self._h).decode()}")
+
+    def last_host_path(self) -> int:
+        """nttmul_last_host_path: 0 staged, 1 direct DMA, 2 zero-copy, -1 no call yet."""
+        return int(self._lib.nttmul_last_host_path(self._h))
+
+    def kernel_name(self, word_bits: int = 0) -> str:
+        """The device kernel(s) a product call dispatches to (nttmul_kernel_name), e.g.
+        "k_rows<Arith32P3,u32,u32,12,0>"."""
+        word_bits = word_bits or (32 if self.q < (1 << 32) else 64)
+        buf = ctypes.create_string_buffer(256)
+        st = self._lib.nttmul_kernel_name(self._h, word_bits, buf, len(buf))
+        if st < 0:
+            self._check(st)
+        return buf.value.decode()
 
     @property
     def io_dtype(self):

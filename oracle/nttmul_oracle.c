@@ -812,6 +812,29 @@ double orc_product_batch(const orc_plan *P, int gs, uint64_t *c, const uint64_t 
   return (t1.tv_sec - t0.tv_sec) + (t1.tv_nsec - t0.tv_nsec) * 1e-9;
 }
 
+/* C1 (BASELINE.json configs[0]): ONE product on ONE core, timed the way time_testing256.c:147-187
+ * times ntt256_product4 -- reps iterations, the inputs restored before each (untimed, :110-116),
+ * CLOCK_MONOTONIC around the product call only (:178-181), the average returned in seconds.
+ * gs = 0: the unoptimized CT sequence (ntt256.C:5-13, orc_product1); 1: GS (ntt256.C:16-24). */
+double orc_time_single(const orc_plan *P, int gs, uint64_t *c, const uint64_t *a,
+                       const uint64_t *b, int reps) {
+  uint32_t n = P->n;
+  uint64_t *sa = (uint64_t *)malloc(n * 8), *sb = (uint64_t *)malloc(n * 8);
+  double total = 0.0;
+  for (int r = 0; r < reps; r++) {
+    memcpy(sa, a, n * 8);
+    memcpy(sb, b, n * 8);
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    if (gs) orc_product4(P, c, sa, sb); else orc_product1(P, c, sa, sb);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    total += (t1.tv_sec - t0.tv_sec) + (t1.tv_nsec - t0.tv_nsec) * 1e-9;
+  }
+  free(sa);
+  free(sb);
+  return reps > 0 ? total / reps : 0.0;
+}
+
 int orc_num_threads(void) {
 #ifdef _OPENMP
   return omp_get_max_threads();

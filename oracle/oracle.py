@@ -80,6 +80,9 @@ def _load() -> ctypes.CDLL:
     lib.orc_product_batch.argtypes = [ctypes.c_void_p, ctypes.c_int, _u64p, _u64p, _u64p,
                                       ctypes.c_uint64, ctypes.c_int]
     lib.orc_num_threads.restype = ctypes.c_int
+    lib.orc_time_single.restype = ctypes.c_double
+    lib.orc_time_single.argtypes = [ctypes.c_void_p, ctypes.c_int, _u64p, _u64p, _u64p,
+                                    ctypes.c_int]
     return lib
 
 
@@ -190,6 +193,16 @@ class Plan:
         sec = self._lib.orc_fast_batch_u32(self._p, _p32(c), _p32(a), _p32(b), cnt, threads)
         if sec < 0:
             raise ValueError("fast_batch_u32 needs q < 2^31")
+        return c, sec
+
+    def time_single(self, a, b, gs: bool = False, reps: int = 30):
+        """One product on one core, timed as time_testing256.c:147-187 (inputs restored untimed
+        before each of `reps` calls, CLOCK_MONOTONIC around the call); returns (c, seconds per
+        product).  gs=False: the unoptimized CT sequence ntt256.C:5-13."""
+        a = np.ascontiguousarray(a, dtype=np.uint64)
+        b = np.ascontiguousarray(b, dtype=np.uint64)
+        c = np.zeros(self.n, dtype=np.uint64)
+        sec = self._lib.orc_time_single(self._p, int(gs), _p64(c), _p64(a), _p64(b), reps)
         return c, sec
 
     def product_batch(self, a: np.ndarray, b: np.ndarray, gs: bool = True, threads: int = 0):

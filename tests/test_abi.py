@@ -59,3 +59,22 @@ def test_no_device_host_alloc():
     with pytest.raises(nttmul.NttmulError) as ei:
         nttmul.host_empty((4, 16), "uint32")
     assert ei.value.status == nttmul.NTTMUL_ENODEV
+
+
+@pytest.mark.parametrize("flag", ["NTTMUL_ABL_NOLOAD", "NTTMUL_ABL_NOXCHG", "NTTMUL_ABL_NOSTORE",
+                                  "NTTMUL_ABL_TWMASK", "NTTMUL_KBENCH_LITE", "NTTMUL_ABL_L2LOAD"])
+def test_ablation_switches_refuse_library_build(flag):
+    """The wrong-result kbench ablation switches cannot reach libnttmul.so: kernels.hip stops with
+    #error unless NTTMUL_KBENCH_BUILD is also defined (tools/kbench/build.sh only)."""
+    src = os.path.join(nttmul.PKG_DIR, "csrc", "kernels.hip")
+    inc = ["-I" + os.path.join(nttmul.PKG_DIR, "csrc"),
+           "-I" + os.path.join(os.path.dirname(nttmul.PKG_DIR), "include")]
+    cmd = ["/opt/rocm/bin/hipcc", "-E", "--offload-arch=gfx950", "-std=c++17", *inc, src,
+           "-o", os.devnull]
+    if not os.path.exists(cmd[0]):
+        pytest.skip("hipcc not present")
+    bad = subprocess.run(cmd + [f"-D{flag}=1"], capture_output=True, text=True)
+    assert bad.returncode != 0 and "wrong-result kbench switches" in bad.stderr
+    ok = subprocess.run(cmd + [f"-D{flag}=1", "-DNTTMUL_KBENCH_BUILD=1"], capture_output=True,
+                        text=True)
+    assert ok.returncode == 0, ok.stderr[-2000:]

@@ -98,3 +98,29 @@ def test_power_probe_summary():
     assert out["ppt_limiter_active"] == f"{out['busy_samples']}/{out['busy_samples']}"
     assert bench.power_probe(lambda: None, lambda: None, 0.01, None) is None
     assert bench.power_reader("", 0) is None or callable(bench.power_reader("", 0)[0])
+
+
+def test_host_cores_rule(monkeypatch):
+    """cpu_baseline's thread count: every core of the affinity mask, capped by the cgroup quota
+    and OMP_NUM_THREADS (each reported beside the choice)."""
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    c = bench.host_cores()
+    assert c["threads"] == min(x for x in (c["sched_getaffinity"], c["cgroup_cpu_quota"], 3) if x)
+    assert c["OMP_NUM_THREADS"] == 3 and c["os_cpu_count"] >= c["sched_getaffinity"] >= 1
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    c = bench.host_cores()
+    assert c["OMP_NUM_THREADS"] is None and c["threads"] <= c["sched_getaffinity"]
+
+
+def test_c1_single_product_line():
+    """BASELINE configs[0] (C1): one unoptimized-CT product on one core, checked vs the oracle."""
+    c1 = bench.c1_single(target_s=0.05)
+    assert c1["matches_oracle"] and c1["cores"] == 1 and c1["n"] == 1024
+    assert c1["q"] == 2013265921 and c1["value"] > 0
+    assert c1["us_per_polymult"] == pytest.approx(1e6 / c1["value"])
+
+
+def test_weak_scaling_batch_is_constant():
+    """--batch-per-gpu is the same at every N (no switch to C4's slice at 8 ranks)."""
+    assert bench.parse([]).batch_per_gpu == 65536
+    assert bench.parse(["--gpus", "8"]).batch_per_gpu == 65536

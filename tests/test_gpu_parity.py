@@ -42,6 +42,10 @@ def _ctx(n, q, psi=0, **kw):
 def test_native_library_is_loaded_and_on_gpu(torch_cuda):
     ctx = _ctx(4096, Q31)
     assert ctx.info.ndev >= 1 and ctx.word_bits == 32 and ctx.info.kernel == 1
+    # the kernel the bench line names is the dispatched one (D = 3 blocks at n = 4096)
+    assert ctx.kernel_name(32) == "k_rows<Arith32P3,u32,u32,12,0>"
+    assert ctx.kernel_name(64) == "k_rows<Arith32P3,u64,u64,12,0>"
+    assert _ctx(1024, Q31).kernel_name() == "k_rows<Arith32P,u32,u32,10,0>"
     assert os.path.samefile(nttmul.LIB_PATH, nttmul.load_library()._name)
 
 
@@ -328,16 +332,29 @@ def test_single_multiply_entry(torch_cuda):
     assert np.array_equal(c.astype(np.uint64), O.Plan(4096, Q31).product_merged(a[0], b[0]))
 
 
-def test_multi_device_context_split(torch_cuda):
-    torch = torch_cuda
-    if torch.cuda.device_count() < 2:
-        pytest.skip("needs 2 GPUs")
-    ctx = _ctx(2048, Q31, ndev=2)
-    a, b = O.fill_inputs(2048, Q31, 0, 9)
-    c = ctx.multiply(a.astype(np.uint32), b.astype(np.uint32)).astype(np.uint64)
-    P = O.Plan(2048, Q31)
-    for i in range(9):
-        assert np.array_equal(c[i], P.product_merged(a[i], b[i]))
+@pytest.mark.parametrize("n,q,ndev,batch", [(2048, Q31, 2, 9), (4096, Q31, 2, 1537),
+                                             (4096, Q31, 3, 3001), (65536, Q62, 2, 9),
+                                             (1024, Q62, 4, 2049)])
+def test_multi_device_context_split(n, q, ndev, batch, torch_cuda):
+    """The host-buffer call split over `ndev` context devices, each slice driven by its own host
+    thread (nttmul.cpp run_host).  NTTMUL_FLAG_SHARE_DEVICES maps the slices round-robin over the
+    visible devices, so on a one-GPU box every slice shares it (own streams, slots and scratch);
+    with ndev real GPUs each slice gets its own.  Every product is checked, staged and direct."""
+    ctx = _ctx(n, q, ndev=ndev, share_devices=True)
+    assert ctx.info.ndev == ndev
+    a, b = O.fill_inputs(n, q, 5, batch)
+    dt = np.uint32 if q < (1 << 32) else np.uint64
+    ref = O.Plan(n, q).product_batch(a, b)[0].reshape(batch, n)
+    c = ctx.multiply(a.astype(dt), b.astype(dt)).astype(np.uint64)
+    assert np.array_equal(c, ref)
+    assert ctx.last_host_path() in (0, 2)
+    ap, bp, cp = (nttmul.host_empty((batch, n), dt) for _ in range(3))
+    ap[...] = a
+    bp[...] = b
+    cp[...] = 0
+    ctx.multiply(ap, bp, out=cp)
+    assert ctx.last_host_path() == 1
+    assert np.array_equal(cp.astype(np.uint64), ref)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -476,10 +493,19 @@ def test_host_path_pinned_direct(n, q, batch, torch_cuda):
     bp[...] = b
     cp[...] = 0
     assert ctx.multiply(ap, bp, out=cp) is cp
+    assert ctx.last_host_path() == 1                  # the direct-DMA branch really ran
     ref = O.Plan(n, q).product_batch(a, b)[0].reshape(batch, n)
     assert np.array_equal(cp.astype(np.uint64), ref)
     mixed = ctx.multiply(ap, b.astype(dt))            # c pageable: staged
+    assert ctx.last_host_path() == 0
     assert np.array_equal(mixed.astype(np.uint64), ref)
+    # operands that are views into one larger pinned block (each range inside that allocation)
+    big = nttmul.host_empty((2 * batch, n), dt)
+    big[:batch] = a
+    big[batch:] = b
+    c2 = nttmul.host_empty((batch, n), dt)
+    ctx.multiply(big[:batch], big[batch:], out=c2)
+    assert np.array_equal(c2.astype(np.uint64), ref) and ctx.last_host_path() == 1
 
 
 # ---------------------------------------------------------------------------------------------

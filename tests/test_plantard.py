@@ -16,8 +16,10 @@ import random
 import pytest
 
 M64 = 1 << 64
-# the benchmark modulus, both ends of the Arith32P range, and a mid-range NTT prime
-QS = [2013265921, 2147352577, 1073872897, 1811939329]
+# the benchmark modulus, both ends of the 2^30..2^31 range, a mid-range NTT prime, and the small
+# moduli the dispatcher also sends to Arith32P (the reference's 12289, the FPGA's 7681, ~2^20, ~2^29)
+QS = [2013265921, 2147352577, 1073872897, 1811939329,
+      12289, 7681, 1032193, 536813569]   # small and mid-size q: Arith32P serves every q < 2^31
 
 
 def pair(w, q, signed=False):

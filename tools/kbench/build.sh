@@ -9,7 +9,7 @@ OUT=$R/tools/kbench/bin
 mkdir -p $OUT
 build() {
   local name=$1; shift
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -I$R/include -I$P/csrc -DVARIANT="\"$name\"" ${KB_FLAGS:--DNTTMUL_KBENCH_LITE=1} "$@" \
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -I$R/include -I$P/csrc -DNTTMUL_KBENCH_BUILD=1 -DVARIANT="\"$name\"" ${KB_FLAGS:--DNTTMUL_KBENCH_LITE=1} "$@" \
     $R/tools/kbench/kbench.cpp $P/csrc/kernels.hip $P/csrc/planner.cpp -o $OUT/kbench_$name &
 }
 if [ $# -eq 0 ]; then set -- base; fi
