@@ -94,7 +94,8 @@
 // tools/kbench timing binaries (tools/kbench/build.sh passes NTTMUL_KBENCH_BUILD), never into
 // libnttmul.so
 #if (NTTMUL_ABL_TWMASK || NTTMUL_ABL_NOLOAD || NTTMUL_ABL_NOXCHG || NTTMUL_ABL_NOSTORE || \
-     NTTMUL_KBENCH_LITE || defined(NTTMUL_ABL_L2LOAD)) && !defined(NTTMUL_KBENCH_BUILD)
+     NTTMUL_KBENCH_LITE || defined(NTTMUL_ABL_L2LOAD) || defined(NTTMUL_STAGGER)) && \
+    !defined(NTTMUL_KBENCH_BUILD)
 #error "NTTMUL_ABL_* / NTTMUL_KBENCH_LITE are wrong-result kbench switches (tools/kbench/build.sh only)"
 #endif
 
@@ -569,6 +570,10 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
   const size_t base_r = base_l;
 #endif
 
+#ifdef NTTMUL_STAGGER  // kbench experiment: one-wave blocks of generation blockIdx / 1024 wait
+  if constexpr (LOGS == 10 && L1 == 0)
+    for (unsigned i = 0; i < (blockIdx.x >> 10) * NTTMUL_STAGGER; i++) __builtin_amdgcn_s_sleep(8);
+#endif
   W x[16], y[16];
   // NTTMUL_CPOL >= 0: a, b, c of a one-product-per-block u32 product through buffer loads /
   // stores (descriptor from block-uniform values, 32-bit per-lane offsets, nt by default)
@@ -765,6 +770,219 @@ __global__ __launch_bounds__(256) void k_cols_inv(KParams<A> P,
 }
 
 // ---------------------------------------------------------------------------------------------
+// Persistent, phase-pipelined multi-pass product (n = 2^L1 * 4096 > 4096)
+// ---------------------------------------------------------------------------------------------
+// The three passes of multipass_l1 (k_cols_fwd -> k_rows<..., 12, L1> -> k_cols_inv) as tasks of
+// ONE launch: a grid of resident workgroups pulls tickets from a device-side counter.  Per
+// polynomial p there are kMpCols column-forward tasks CF(p, s) (256 columns each, all 2^L1
+// elements of each column), 2^L1 row tasks R(p, r) and kMpCols column-inverse tasks CI(p, s).
+// R(p, .) needs every CF(p, .), CI(p, .) every R(p, .).  Ticket t belongs to step k = t / T with
+// T = 2 kMpCols + 2^L1 tasks: first the CI tasks of polynomial k - 2 lag, then the R tasks of
+// k - lag, then the CF tasks of k.  A task's dependencies therefore hold smaller tickets, which
+// were handed to running workgroups earlier: the smallest unfinished ticket can always run, so
+// the schedule cannot deadlock, and with lag steps between producer and consumer the wait is
+// normally over before the consumer starts.  No relaunch, no grid-wide ramp and drain between
+// passes; the memory-bound column tasks of younger polynomials run beside the VALU-bound row tasks
+// of older ones on the same CUs, and an intermediate is read back about 2 lag steps (~2 lag x
+// 1.5 MiB for C5) after it was written, while it is still in the 256 MiB Infinity Cache.
+//
+// Hand-off (MI355X_MICROARCH.md §inter-workgroup visibility, table row 1): every intermediate is
+// stored with sc1 stores (write-through; a cross-XCD reader then cannot see a stale copy in its
+// own L2 once the data reached memory) and read with sc1 loads (L1 bypassed); each storing wave
+// waits vmcnt(0), the workgroup barriers, and one lane adds 1 (agent scope) to the polynomial's
+// counter; a consumer's lane 0 polls that counter with sc1 loads, then the workgroup barriers.
+// Every scratch word is written once and read once per launch (no address reuse inside a
+// launch).  A poll that has not seen its count after ~2^24 polls (far beyond any wait of a
+// correct schedule) records a fault flag and gives up, so a bug ends the launch instead of
+// hanging the GPU.
+constexpr int kMpCols = 16;  // column tasks per polynomial: 4096 columns / 256 threads
+struct MpSync {
+  unsigned *head;            // ticket counter (zeroed before the launch)
+  unsigned *cnt;             // [2][batch]: finished CF / R tasks per polynomial (zeroed)
+  unsigned *fault;           // set when a poll gave up
+  unsigned lag;              // steps between a polynomial's CF, R and CI tasks
+  unsigned long long *stats; // tools/kbench NTTMUL_MP_STATS builds: per task type (CI, R, CF)
+                             // [0..2] busy ticks, [3..5] wait ticks, [6..8] tasks (100 MHz clock)
+};
+#ifndef NTTMUL_MP_STATS
+#define NTTMUL_MP_STATS 0
+#endif
+#if NTTMUL_MP_STATS && !defined(NTTMUL_KBENCH_BUILD)
+#error "NTTMUL_MP_STATS is a tools/kbench instrumentation switch"
+#endif
+// sc1 hand-off policy of the intermediates (2 = sc1 loads and stores; kbench A/B only: 0 plain)
+#ifndef NTTMUL_MP_POL
+#define NTTMUL_MP_POL 2
+#endif
+#if NTTMUL_MP_POL != 2 && !defined(NTTMUL_KBENCH_BUILD)
+#error "NTTMUL_MP_POL != 2 breaks the hand-off protocol (tools/kbench A/B only)"
+#endif
+
+template <int POL, class T>
+__device__ __forceinline__ T ld_pol(const T *p) {
+  if constexpr (POL == 2) return __hip_atomic_load((T *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else if constexpr (POL == 1) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <int POL, class T>
+__device__ __forceinline__ void st_pol(T *p, T v) {
+  if constexpr (POL == 2) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else if constexpr (POL == 1) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+// the storing workgroup's release: every wave's stores complete, then one lane counts the task
+__device__ __forceinline__ void mp_publish(unsigned *cnt) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// the consuming workgroup's wait for `need` finished producer tasks
+__device__ __forceinline__ void mp_wait(const MpSync &S, const unsigned *cnt, unsigned need) {
+  if (threadIdx.x == 0) {
+    unsigned polls = 0;
+    while (__hip_atomic_load((unsigned *)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++polls == (1u << 24)) {
+        __hip_atomic_store(S.fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void mp_stat(const MpSync &S, int kind, unsigned long long t0,
+                                        unsigned long long t1) {
+  if (NTTMUL_MP_STATS && threadIdx.x == 0) {
+    const unsigned long long t2 = __builtin_amdgcn_s_memrealtime();
+    atomicAdd(S.stats + kind, t2 - t1);
+    atomicAdd(S.stats + 3 + kind, t1 - t0);
+    atomicAdd(S.stats + 6 + kind, 1ull);
+  }
+}
+
+template <class A, class IO, int L1>
+__global__ __launch_bounds__(256) void k_mp_persist(KParams<A> P, const IO *__restrict__ a,
+                                                    const IO *__restrict__ b, IO *__restrict__ c,
+                                                    typename A::word *__restrict__ ta,
+                                                    typename A::word *__restrict__ tb,
+                                                    typename A::word *__restrict__ tc,
+                                                    unsigned batch, MpSync S) {
+  using W = typename A::word;
+  constexpr int LOGS = 12, NR = 1 << L1, M = 1 << L1;
+  using Gr = Groups<LOGS>;
+  constexpr int N = Gr::N, G = Gr::G, NP = Gr::NP;
+  constexpr unsigned T = 2 * kMpCols + NR;
+  constexpr size_t kPoly = (size_t)N << L1;   // words per polynomial
+  __shared__ W lds[NP];
+  __shared__ unsigned s_ticket;
+  const int j = threadIdx.x;
+  const unsigned total = (batch + 2 * S.lag) * T;
+  if (j == 0) s_ticket = __hip_atomic_fetch_add(S.head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  unsigned t = s_ticket;
+  while (t < total) {
+    __syncthreads();  // every lane has read s_ticket
+    if (j == 0) s_ticket = __hip_atomic_fetch_add(S.head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned k = t / T, r = t % T;
+    if (r < kMpCols) {
+      // CI(p, r): inverse column stages L1-1 .. 0 with F folded into stage 0, canonical output
+      if (k >= 2 * S.lag && k - 2 * S.lag < batch) {
+        const size_t p = k - 2 * S.lag;
+        const unsigned long long t0 = NTTMUL_MP_STATS ? __builtin_amdgcn_s_memrealtime() : 0;
+        mp_wait(S, S.cnt + batch + p, NR);
+        const unsigned long long t1 = NTTMUL_MP_STATS ? __builtin_amdgcn_s_memrealtime() : 0;
+        const size_t base = p * kPoly + (size_t)r * 256 + j;
+        W x[M];
+#pragma clang loop unroll(full)
+        for (int m = 0; m < M; m++) x[m] = ld_pol<NTTMUL_MP_POL>(tc + base + ((size_t)m << LOGS));
+#pragma clang loop unroll(full)
+        for (int st = L1 - 1; st >= 0; st--) {
+          const int dist = M >> (st + 1);
+#pragma clang loop unroll(full)
+          for (int m = 0; m < M; m++) {
+            if (m & dist) continue;
+            if (st == 0) {
+              P.ar.gs_scaled(x[m], x[m + dist], P.f, P.fs, P.wf, P.wfs);
+            } else {
+              const TwPair<W> tw = P.iw[(1 << st) + (m >> (L1 - st))];
+              P.ar.gs(x[m], x[m + dist], tw.w, tw.ws);
+            }
+          }
+        }
+#pragma clang loop unroll(full)
+        for (int m = 0; m < M; m++)
+          st_pol<1>(c + base + ((size_t)m << LOGS), (IO)(A::kInvCanonical ? x[m] : P.ar.canon(x[m])));
+        if (NTTMUL_MP_STATS) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __syncthreads();
+          mp_stat(S, 0, t0, t1);
+        }
+      }
+    } else if (r < kMpCols + NR) {
+      // R(p, row): row stages L1 .. L1 + 11, base multiplication, inverse row stages; lazy out
+      if (k >= S.lag && k - S.lag < batch) {
+        const size_t p = k - S.lag;
+        const int row = (int)(r - kMpCols);
+        const unsigned long long t0 = NTTMUL_MP_STATS ? __builtin_amdgcn_s_memrealtime() : 0;
+        mp_wait(S, S.cnt + p, kMpCols);
+        const unsigned long long t1 = NTTMUL_MP_STATS ? __builtin_amdgcn_s_memrealtime() : 0;
+        const size_t base = p * kPoly + ((size_t)row << LOGS) + Gr::base(0, j);
+        W x[16], y[16];
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+          x[q] = ld_pol<NTTMUL_MP_POL>(ta + base + Gr::off(0, q));
+          y[q] = ld_pol<NTTMUL_MP_POL>(tb + base + Gr::off(0, q));
+        }
+        constexpr int D = NTTMUL_BASE_D ? A::kBaseD : 0;
+        TwPair<W> zw[16];
+        fwd_all<A, LOGS, 0, 2, D>(P.ar, x, y, lds, lds, P.fw, j, row, L1, zw);
+        base_mult<A, LOGS, D>(P.ar, x, y, zw);
+        inv_all<A, LOGS, G - 1, false, D>(P, x, y, lds, lds, P.iw, j, row, L1);
+#pragma unroll
+        for (int q = 0; q < 16; q++) st_pol<NTTMUL_MP_POL>(tc + base + Gr::off(0, q), x[q]);
+        mp_publish(S.cnt + batch + p);
+        mp_stat(S, 1, t0, t1);
+      }
+    } else {
+      // CF(p, s): forward column stages 0 .. L1-1 of a and b
+      if (k < batch) {
+        const size_t p = k;
+        const unsigned long long t0 = NTTMUL_MP_STATS ? __builtin_amdgcn_s_memrealtime() : 0;
+        const size_t base = p * kPoly + (size_t)(r - kMpCols - NR) * 256 + j;
+        W x[M], y[M];
+#pragma clang loop unroll(full)
+        for (int m = 0; m < M; m++) {
+          x[m] = (W)ld_pol<NTTMUL_NT_COLS>(a + base + ((size_t)m << LOGS));
+          y[m] = (W)ld_pol<NTTMUL_NT_COLS>(b + base + ((size_t)m << LOGS));
+        }
+#pragma clang loop unroll(full)
+        for (int st = 0; st < L1; st++) {
+          const int dist = M >> (st + 1);
+#pragma clang loop unroll(full)
+          for (int m = 0; m < M; m++) {
+            if (m & dist) continue;
+            const TwPair<W> tw = P.fw[(1 << st) + (m >> (L1 - st))];
+            P.ar.ct(x[m], x[m + dist], tw.w, tw.ws);
+            P.ar.ct(y[m], y[m + dist], tw.w, tw.ws);
+          }
+        }
+#pragma clang loop unroll(full)
+        for (int m = 0; m < M; m++) {
+          st_pol<NTTMUL_MP_POL>(ta + base + ((size_t)m << LOGS), x[m]);
+          st_pol<NTTMUL_MP_POL>(tb + base + ((size_t)m << LOGS), y[m]);
+        }
+        mp_publish(S.cnt + p);
+        mp_stat(S, 2, t0, t0);
+      }
+    }
+    __syncthreads();  // s_ticket written by lane 0 above
+    t = s_ticket;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Synthetic inputs and input validation
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
@@ -909,9 +1127,54 @@ static hipError_t multipass_l1(const LaunchTables &T, const void *a, const void 
   return hipGetLastError();
 }
 
+// The same product as multipass_l1 in one persistent launch (k_mp_persist).  scr[3]: the
+// ticket / counter words, mp_sync_bytes(batch), zeroed here on the stream before the launch.
+template <class A, class IO, int L1>
+static hipError_t multipass_persist(const LaunchTables &T, const void *a, const void *b, void *c,
+                                    size_t batch, void **scr, hipStream_t s) {
+  using W = typename A::word;
+  if (tl_describe) {
+    describe_add(std::string("k_mp_persist<") + AName<A>::v + "," + word_name<IO>() + "," +
+                 std::to_string(L1) + ">");
+    return hipSuccess;
+  }
+  if (batch == 0) return hipSuccess;
+  if (batch > 0x7FFFFFFFull / (2 * kMpCols + (1 << L1))) return hipErrorInvalidValue;
+  static int per_cu = 0;  // resident workgroups per CU (occupancy of this instantiation)
+  if (!per_cu) {
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, reinterpret_cast<const void *>(&k_mp_persist<A, IO, L1>), 256, 0);
+    if (e != hipSuccess || per_cu < 1) per_cu = 1;
+  }
+  const KParams<A> P = product_params<A>(T);
+  unsigned *sw = (unsigned *)scr[3];
+  hipError_t e = hipMemsetAsync(sw, 0, mp_sync_bytes(batch), s);
+  if (e != hipSuccess) return e;
+  MpSync S;
+  S.head = sw;
+  S.fault = sw + 1;
+  S.cnt = sw + 2;
+  S.lag = (unsigned)T.mp_lag;
+  S.stats = (unsigned long long *)T.mp_stats;
+  const unsigned grid = (unsigned)(per_cu * (T.cus > 0 ? T.cus : 256));
+  hipLaunchKernelGGL((k_mp_persist<A, IO, L1>), dim3(grid), dim3(256), 0, s, P, (const IO *)a,
+                     (const IO *)b, (IO *)c, (W *)scr[0], (W *)scr[1], (W *)scr[2],
+                     (unsigned)batch, S);
+  return hipGetLastError();
+}
+
 template <class A, class IO>
 static hipError_t multipass(const LaunchTables &T, const void *a, const void *b, void *c,
                             size_t batch, void **scr, hipStream_t s) {
+  if (T.mp_lag > 0 && scr[3] && !(T.logn == 16 && NTTMUL_SPLIT16 == 5)) {
+    switch (T.logn) {
+      case 13: return multipass_persist<A, IO, 1>(T, a, b, c, batch, scr, s);
+      case 14: return multipass_persist<A, IO, 2>(T, a, b, c, batch, scr, s);
+      case 15: return multipass_persist<A, IO, 3>(T, a, b, c, batch, scr, s);
+      case 16: return multipass_persist<A, IO, 4>(T, a, b, c, batch, scr, s);
+      default: return hipErrorInvalidValue;
+    }
+  }
   switch (T.logn) {
     case 13: return multipass_l1<A, IO, 1>(T, a, b, c, batch, scr[0], scr[1], scr[2], s);
     case 14: return multipass_l1<A, IO, 2>(T, a, b, c, batch, scr[0], scr[1], scr[2], s);
@@ -946,7 +1209,7 @@ hipError_t launch_polymul(const LaunchTables &T, const void *a, const void *b, v
                           size_t batch, int io_bits, void **scr, hipStream_t s) {
 #if NTTMUL_KBENCH_LITE == 2  // tools/kbench C5 builds: 64-bit words, n = 65536 only
   if (T.word_bits != 64 || T.logn != 16 || io_bits != 64) return hipErrorNotSupported;
-  return multipass_l1<Arith64, uint64_t, 4>(T, a, b, c, batch, scr[0], scr[1], scr[2], s);
+  return multipass<Arith64, uint64_t>(T, a, b, c, batch, scr, s);
 #elif NTTMUL_KBENCH_LITE  // tools/kbench quick builds: 32-bit words, q < 2^31, n <= 4096 only
   if (T.word_bits != 32 || T.q >= (1ull << 31) || T.logn > 12 || io_bits != 32) return hipErrorNotSupported;
   switch (a32_kind(T.q)) {
@@ -973,7 +1236,7 @@ hipError_t launch_polymul(const LaunchTables &T, const void *a, const void *b, v
 
 hipError_t describe_polymul(const LaunchTables &T, int io_bits, std::string *out) {
   out->clear();
-  void *scr[3] = {nullptr, nullptr, nullptr};
+  void *scr[4] = {nullptr, nullptr, nullptr, (void *)out};  // (non-null: the persistent form)
   tl_describe = out;
   const hipError_t e = launch_polymul(T, nullptr, nullptr, nullptr, 1, io_bits, scr, nullptr);
   tl_describe = nullptr;

@@ -21,10 +21,18 @@ struct LaunchTables {
   const void *fw, *iw;     // forward / inverse twiddle (value, companion) pairs, n entries
                            // (planner.cpp tw_pair: Shoup, or Montgomery form for Arith32)
   int cus;                 // compute units of the device (persistent grid size)
+  int mp_lag;              // n > 4096: 0 = three launches per product (k_cols_fwd, k_rows,
+                           // k_cols_inv); > 0 = one persistent launch (k_mp_persist) with this
+                           // many steps between a polynomial's column, row and inverse tasks
+  void *mp_stats = nullptr;  // tools/kbench NTTMUL_MP_STATS builds: 9 u64 task statistics
 };
 
+// Bytes of the ticket / counter words k_mp_persist needs for `batch` polynomials (scr[3]).
+inline size_t mp_sync_bytes(size_t batch) { return (2 * batch + 2) * sizeof(unsigned); }
+
 // c = a * b for `batch` polynomials of n = 2^logn words of io_bits (32/64) each, on stream s.
-// scr: three device buffers of batch * n words of word_bits, used only when n > 4096.
+// scr: three device buffers of batch * n words of word_bits, used only when n > 4096, and a
+// fourth of mp_sync_bytes(batch) for the persistent form (T.mp_lag > 0; nullptr: three launches).
 hipError_t launch_polymul(const LaunchTables &T, const void *a, const void *b, void *c,
                           size_t batch, int io_bits, void **scr, hipStream_t s);
 // The kernels launch_polymul would launch for (T, io_bits), as "k_rows<Arith32P3,u32,u32,12,0>"

@@ -24,6 +24,10 @@
 
 #include "launch.hpp"
 #include "nttmul.h"
+
+#ifndef NTTMUL_MP_LAG_DEFAULT
+#define NTTMUL_MP_LAG_DEFAULT 0
+#endif
 #include "planner.hpp"
 
 using namespace nttmul;
@@ -41,8 +45,8 @@ constexpr size_t kChunkBytes = 8u << 20;      // host-path chunk, per operand
 // it was enqueued on: two device-API calls on different streams (or two host-path slots) never
 // overwrite each other's intermediates.
 struct Scratch {
-  void *buf[3] = {nullptr, nullptr, nullptr};
-  size_t bytes = 0;
+  void *buf[4] = {nullptr, nullptr, nullptr, nullptr};  // [3]: k_mp_persist's ticket words
+  size_t bytes = 0, sync_bytes = 0;
   void *perm = nullptr;
   size_t perm_bytes = 0;
   hipEvent_t ev = nullptr;                    // recorded after the last enqueued use
@@ -117,6 +121,15 @@ int fail(nttmul_ctx *ctx, hipError_t e, const char *what) {
     if (_e != hipSuccess) return fail(ctx, _e, #expr); \
   } while (0)
 
+// n > 4096 products: NTTMUL_MP_LAG > 0 runs the three passes as one persistent launch
+// (kernels.hip k_mp_persist) with that many steps between a polynomial's column, row and inverse
+// tasks; 0 = three launches.  Default kMpLagDefault.
+constexpr int kMpLagDefault = NTTMUL_MP_LAG_DEFAULT;
+int mp_lag() {
+  const char *e = getenv("NTTMUL_MP_LAG");
+  return e ? std::max(0, atoi(e)) : kMpLagDefault;
+}
+
 LaunchTables tables_for(const nttmul_ctx *ctx, const DevState &d) {
   const Plan &P = ctx->plan;
   LaunchTables T;
@@ -131,6 +144,7 @@ LaunchTables tables_for(const nttmul_ctx *ctx, const DevState &d) {
   T.fw = d.fw;
   T.iw = d.iw;
   T.cus = d.cus;
+  T.mp_lag = mp_lag();
   return T;
 }
 
@@ -187,7 +201,7 @@ int scratch_release(nttmul_ctx *ctx, Scratch &sc, hipStream_t s) {
 
 void scratch_free(Scratch &sc) {
   if (sc.used) (void)hipEventSynchronize(sc.ev);
-  for (void *p : {sc.buf[0], sc.buf[1], sc.buf[2], sc.perm})
+  for (void *p : {sc.buf[0], sc.buf[1], sc.buf[2], sc.buf[3], sc.perm})
     if (p) (void)hipFree(p);
   if (sc.ev) (void)hipEventDestroy(sc.ev);
   sc = Scratch();
@@ -301,6 +315,9 @@ int run_device(nttmul_ctx *ctx, DevState &d, Scratch &sc, int op, void *c, const
   int st = scratch_acquire(ctx, sc, s);
   if (st) return st;
   if (multipass && (st = ensure(ctx, sc, sc.buf, 3, &sc.bytes, chunk * w_poly))) return st;
+  if (multipass && op == OP_MULTIPLY && T.mp_lag > 0 &&
+      (st = ensure(ctx, sc, &sc.buf[3], 1, &sc.sync_bytes, mp_sync_bytes(chunk))))
+    return st;
   if (reorder && (st = ensure(ctx, sc, &sc.perm, 1, &sc.perm_bytes, chunk * io_poly))) return st;
   for (size_t p = 0; p < batch && !st; p += chunk) {
     const size_t cnt = std::min(chunk, batch - p);
@@ -317,6 +334,17 @@ int run_device(nttmul_ctx *ctx, DevState &d, Scratch &sc, int op, void *c, const
       e = launch_bitrev(cp, cp, P.logn, cnt, io_bits, s);
     }
     if (e != hipSuccess) st = fail(ctx, e, "sub-batch launch");
+    // NTTMUL_FLAG_VALIDATE: a persistent multi-pass launch whose dependency poll gave up (a
+    // scheduling bug, never a correct run) is reported instead of returning its output
+    if (!st && multipass && op == OP_MULTIPLY && T.mp_lag > 0 && (ctx->flags & NTTMUL_FLAG_VALIDATE)) {
+      unsigned fault = 0;
+      if ((e = hipMemcpyAsync(&fault, (unsigned *)sc.buf[3] + 1, sizeof(fault),
+                              hipMemcpyDeviceToHost, s)) != hipSuccess ||
+          (e = hipStreamSynchronize(s)) != hipSuccess)
+        st = fail(ctx, e, "persistent fault flag");
+      else if (fault)
+        st = fail(ctx, hipErrorLaunchFailure, "k_mp_persist: a dependency wait gave up");
+    }
   }
   const int rel = scratch_release(ctx, sc, s);
   return st ? st : rel;

@@ -184,13 +184,20 @@ def test_random_prime_sweep_multipass(n, torch_cuda):
             assert np.array_equal(c[i], P.product_merged(a[i], b[i])), (n, q, i)
 
 
+MP_LAGS = [0, 32]   # NTTMUL_MP_LAG: three launches / the persistent k_mp_persist
+
+
+@pytest.mark.parametrize("lag", MP_LAGS)
 @pytest.mark.parametrize("n", [8192, 16384, 32768, 65536])
 @pytest.mark.parametrize("q", [Q31, Q30, Q32, Q62, Q31HI, Q31LO])
-def test_multipass_vs_oracle(n, q, torch_cuda):
+def test_multipass_vs_oracle(n, q, lag, torch_cuda, monkeypatch):
     """n > 4096: column pass + fused rows + inverse column pass, ragged batch of 3 (and 17 at
-    n = 8192) against the restated reference product (OpenMP batch) and evaluation at roots."""
+    n = 8192) against the restated reference product (OpenMP batch) and evaluation at roots;
+    as three launches and as one persistent launch (lag 32 > the batch: the whole product is
+    pipeline fill and drain)."""
+    monkeypatch.setenv("NTTMUL_MP_LAG", str(lag))
     P = O.Plan(n, q)
-    ctx = _ctx(n, q)
+    ctx = _ctx(n, q, validate=True)
     assert ctx.info.kernel == 2
     for batch in ((3, 17) if n == 8192 else (3,)):
         a, b = O.fill_inputs(n, q, 7 + batch, batch)
@@ -243,20 +250,27 @@ def _check_whole_batch(n, q, word_bits, p0, count, a, b, c, chunk=8192):
     return checked
 
 
-@pytest.mark.parametrize("n,q,word_bits,batch,chunk_mb,lanes", [
-    (4096, Q31, 32, 65536, None, None), (1024, Q31, 32, 4096, None, None),
-    (65536, Q62, 64, 1024, None, None), (65536, Q62, 64, 1024, 64, 2),
-    (8192, Q31, 32, 2500, 32, None)])
-def test_full_size_device_path(n, q, word_bits, batch, chunk_mb, lanes, torch_cuda, monkeypatch):
+@pytest.mark.parametrize("n,q,word_bits,batch,chunk_mb,lanes,lag", [
+    (4096, Q31, 32, 65536, None, None, None), (1024, Q31, 32, 4096, None, None, None),
+    (65536, Q62, 64, 1024, None, None, 0), (65536, Q62, 64, 1024, None, None, 32),
+    (65536, Q62, 64, 1024, None, None, 4), (65536, Q62, 64, 1024, 64, 2, None),
+    (65536, Q62, 64, 1024, 96, None, 32), (8192, Q31, 32, 2500, 32, None, None),
+    (16384, Q31, 32, 3000, None, None, 32)])
+def test_full_size_device_path(n, q, word_bits, batch, chunk_mb, lanes, lag, torch_cuda,
+                               monkeypatch):
     """BASELINE configs C3, C2 and C5 at full size on device-resident data, C5 also in 8
     multi-pass sub-batches over the two pipeline lanes and n = 8192 in three serial sub-batches
-    (NTTMUL_MP_CHUNK_MB / NTTMUL_MP_LANES): every product against the oracle, bit-exact."""
+    (NTTMUL_MP_CHUNK_MB / NTTMUL_MP_LANES); C5 both as three launches per product and as one
+    persistent launch (NTTMUL_MP_LAG; lag 4: consumers usually wait for their producers), also
+    in sub-batches: every product against the oracle, bit-exact."""
     torch = torch_cuda
     if chunk_mb:
         monkeypatch.setenv("NTTMUL_MP_CHUNK_MB", str(chunk_mb))
     if lanes:
         monkeypatch.setenv("NTTMUL_MP_LANES", str(lanes))
-    ctx = _ctx(n, q)
+    if lag is not None:
+        monkeypatch.setenv("NTTMUL_MP_LAG", str(lag))
+    ctx = _ctx(n, q, validate=lag is not None)
     dt = _torch_dtype(torch, word_bits)
     a = torch.empty(batch * n, dtype=dt, device="cuda")
     b = torch.empty_like(a)
@@ -289,14 +303,15 @@ def test_c4_last_rank_slice(torch_cuda):
     assert _check_whole_batch(n, q, 32, p0, count, a, b, c) == count
 
 
-@pytest.mark.parametrize("lanes", [1, 2])
-def test_device_calls_on_two_streams(lanes, torch_cuda, monkeypatch):
+@pytest.mark.parametrize("lanes,lag", [(1, 0), (2, 0), (1, 32)])
+def test_device_calls_on_two_streams(lanes, lag, torch_cuda, monkeypatch):
     """Two multi-pass products enqueued back to back on two different streams share the
     context's scratch (nttmul.cpp Scratch, event-ordered) or, with NTTMUL_MP_LANES=2, its
     pipeline lanes (run_lanes: each call's two sub-batches run after its own stream and join
     back into it)."""
     torch = torch_cuda
     monkeypatch.setenv("NTTMUL_MP_LANES", str(lanes))
+    monkeypatch.setenv("NTTMUL_MP_LAG", str(lag))
     n, q, batch = 16384, Q31, 1200
     ctx = _ctx(n, q)
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()

@@ -26,13 +26,15 @@ int main(int argc, char **argv) {
   if (nttmul::make_plan(n, q, 0, &P)) { fprintf(stderr, "bad plan\n"); return 1; }
   int io_bits = argc > 5 ? atoi(argv[5]) : (q < (1ull << 32) ? 32 : 64);
   size_t wb = io_bits / 8, bytes = batch * n * wb;
-  void *a, *b, *c, *fw, *iw, *scr[3] = {0, 0, 0};
+  void *a, *b, *c, *fw, *iw, *scr[4] = {0, 0, 0, 0};
   CK(hipMalloc(&a, bytes)); CK(hipMalloc(&b, bytes)); CK(hipMalloc(&c, bytes));
   CK(hipMalloc(&fw, P.fw.size())); CK(hipMalloc(&iw, P.iw.size()));
   CK(hipMemcpy(fw, P.fw.data(), P.fw.size(), hipMemcpyHostToDevice));
   CK(hipMemcpy(iw, P.iw.data(), P.iw.size(), hipMemcpyHostToDevice));
-  if (P.logn > 12)
-    for (auto &s : scr) CK(hipMalloc(&s, batch * n * (P.word_bits / 8)));
+  if (P.logn > 12) {
+    for (int i = 0; i < 3; i++) CK(hipMalloc(&scr[i], batch * n * (P.word_bits / 8)));
+    CK(hipMalloc(&scr[3], nttmul::mp_sync_bytes(batch)));
+  }
   nttmul::LaunchTables T;
   T.logn = P.logn; T.word_bits = P.word_bits; T.q = P.q; T.qinv_neg = P.qinv_neg;
   T.f = P.f; T.fs = P.fs; T.wf = P.wf; T.wfs = P.wfs; T.fw = fw; T.iw = iw;
@@ -40,7 +42,25 @@ int main(int argc, char **argv) {
   T.f8 = P.f8; T.f8s = P.f8s; T.wf8 = P.wf8; T.wf8s = P.wf8s;
   T.fi = P.fi; T.fis = P.fis; T.wfi = P.wfi; T.wfis = P.wfis; T.r2 = P.r2;
   CK(hipDeviceGetAttribute(&T.cus, hipDeviceAttributeMultiprocessorCount, 0));
+  // KB_MP_LAG > 0: n > 4096 products as one persistent launch (k_mp_persist) with this lag
+  T.mp_lag = getenv("KB_MP_LAG") ? atoi(getenv("KB_MP_LAG")) : 0;
+  if (T.mp_lag > 0 && P.logn > 12) CK(hipMemset(scr[3], 0, nttmul::mp_sync_bytes(batch)));
+  unsigned long long *stats = nullptr;
+#if NTTMUL_MP_STATS
+  CK(hipMalloc(&stats, 9 * 8));
+  CK(hipMemset(stats, 0, 9 * 8));
+  T.mp_stats = stats;
+#endif
   CK(nttmul::launch_fill(a, b, P.logn, q, 0x4E54544D554Cull, 0, batch, io_bits, 0));
+  // KB_ROTATE=R: the timed launches cycle over R (a, b, c) sets with identical inputs, so a batch
+  // smaller than the 256 MiB Infinity Cache is read from HBM (as bench.py --rotate)
+  const int rot = getenv("KB_ROTATE") ? atoi(getenv("KB_ROTATE")) : 1;
+  void *ra[64], *rb[64], *rc[64];
+  ra[0] = a; rb[0] = b; rc[0] = c;
+  for (int i = 1; i < rot && i < 64; i++) {
+    CK(hipMalloc(&ra[i], bytes)); CK(hipMalloc(&rb[i], bytes)); CK(hipMalloc(&rc[i], bytes));
+    CK(nttmul::launch_fill(ra[i], rb[i], P.logn, q, 0x4E54544D554Cull, 0, batch, io_bits, 0));
+  }
   for (int i = 0; i < 3; i++) CK(nttmul::launch_polymul(T, a, b, c, batch, io_bits, scr, 0));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
@@ -64,6 +84,11 @@ int main(int argc, char **argv) {
   }
   for (int i = 0; i < reps; i++) {
     const int k = nstreams == 2 ? (i & 1) : 0;
+    if (rot > 1) {
+      const int r = i % (rot < 64 ? rot : 64);
+      CK(nttmul::launch_polymul(T, ra[r], rb[r], rc[r], batch, io_bits, scr, st[k]));
+      continue;
+    }
     CK(nttmul::launch_polymul(T, a, b, k ? c2 : c, batch, io_bits, scr, st[k]));
   }
   if (nstreams == 2) {
@@ -85,6 +110,18 @@ int main(int argc, char **argv) {
     CK(hipMemcpy(h, c, bytes, hipMemcpyDeviceToHost));
     for (size_t i = 0; i < cnt; i++) sum = sum * 1099511628211ull + h[i];
     free(h);
+  }
+  unsigned fault = 0;
+  if (T.mp_lag > 0 && P.logn > 12) CK(hipMemcpy(&fault, (unsigned *)scr[3] + 1, 4, hipMemcpyDeviceToHost));
+  if (fault) printf("FAULT: k_mp_persist poll gave up\n");
+  if (stats) {
+    unsigned long long h[9];
+    CK(hipMemcpy(h, stats, sizeof(h), hipMemcpyDeviceToHost));
+    const char *nm[3] = {"CI", "R", "CF"};
+    for (int k = 0; k < 3; k++)
+      if (h[6 + k])
+        printf("  %s: %llu tasks, busy %.2f us, wait %.2f us per task\n", nm[k], h[6 + k],
+               h[k] * 0.01 / h[6 + k], h[3 + k] * 0.01 / h[6 + k]);
   }
   printf("%s n=%u q=%llu batch=%zu io=%d: %.4f ms  %.2f Mpolymul/s  %.1f GB/s (%.1f%% of 8 TB/s)  chk=%016llx\n",
          VARIANT, n, (unsigned long long)q, batch, io_bits, ms, pps / 1e6, gbs, gbs / 80.0, sum);
