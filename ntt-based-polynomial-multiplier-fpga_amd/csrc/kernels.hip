@@ -50,6 +50,10 @@
 #ifndef NTTMUL_NT
 #define NTTMUL_NT 1
 #endif
+// n = 1024: a's loads first and a's forward transform before b's (k_rows kSplitAB)
+#ifndef NTTMUL_SPLIT_AB
+#define NTTMUL_SPLIT_AB 0
+#endif
 // NTTMUL_A32H / NTTMUL_A32_PLANTARD (which 32-bit class takes which q): arith_select.hpp
 // incomplete transforms in the product kernel: the last D = A::kBaseD stages become base
 // multiplications of 2^D-coefficient blocks (0: full transforms + pointwise Montgomery product)
@@ -411,8 +415,21 @@ __device__ __forceinline__ void inv_group(const KParams<A> &P, typename A::word 
   }
 }
 
+// LDS ordering between an exchange's writes and reads: the whole workgroup (SYNC 0), or only the
+// wave (SYNC 1: a wave owns its product and its LDS region; a wave's LDS operations execute in
+// order, so only the compiler must be kept from moving them)
+template <int SYNC>
+__device__ __forceinline__ void xsync() {
+  if constexpr (SYNC == 0) {
+    __syncthreads();
+  } else {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 // Move 16 registers of each region from layout gfrom to layout gto through LDS.
-template <int LOGS, int gfrom, int gto, int NREG, class W>
+template <int LOGS, int gfrom, int gto, int NREG, class W, int SYNC = 0>
 __device__ __forceinline__ void exchange(W (&x)[16], W (&y)[16], W *lds_x, W *lds_y, int j) {
   using Gr = Groups<LOGS>;
 #if NTTMUL_ABL_NOXCHG
@@ -424,16 +441,16 @@ __device__ __forceinline__ void exchange(W (&x)[16], W (&y)[16], W *lds_x, W *ld
   if (lds_regions<W>() == 1 && NREG == 2) {  // one region, the two polynomials in turn
 #pragma unroll
     for (int k = 0; k < 16; k++) lds_x[bw + Gr::template padx<X>(Gr::off(gfrom, k))] = x[k];
-    __syncthreads();
+    xsync<SYNC>();
 #pragma unroll
     for (int k = 0; k < 16; k++) x[k] = lds_x[br + Gr::template padx<X>(Gr::off(gto, k))];
-    __syncthreads();
+    xsync<SYNC>();
 #pragma unroll
     for (int k = 0; k < 16; k++) lds_x[bw + Gr::template padx<X>(Gr::off(gfrom, k))] = y[k];
-    __syncthreads();
+    xsync<SYNC>();
 #pragma unroll
     for (int k = 0; k < 16; k++) y[k] = lds_x[br + Gr::template padx<X>(Gr::off(gto, k))];
-    __syncthreads();
+    xsync<SYNC>();
     return;
   }
 #pragma unroll
@@ -441,16 +458,16 @@ __device__ __forceinline__ void exchange(W (&x)[16], W (&y)[16], W *lds_x, W *ld
     lds_x[bw + Gr::template padx<X>(Gr::off(gfrom, k))] = x[k];
     if (NREG == 2) lds_y[bw + Gr::template padx<X>(Gr::off(gfrom, k))] = y[k];
   }
-  __syncthreads();
+  xsync<SYNC>();
 #pragma unroll
   for (int k = 0; k < 16; k++) {
     x[k] = lds_x[br + Gr::template padx<X>(Gr::off(gto, k))];
     if (NREG == 2) y[k] = lds_y[br + Gr::template padx<X>(Gr::off(gto, k))];
   }
-  __syncthreads();
+  xsync<SYNC>();
 }
 
-template <class A, int LOGS, int g, int NPOLY = 2, int SKIP = 0>
+template <class A, int LOGS, int g, int NPOLY = 2, int SKIP = 0, int SYNC = 0>
 __device__ __forceinline__ void fwd_all(const A &ar, typename A::word (&x)[16],
                                         typename A::word (&y)[16], typename A::word *lx,
                                         typename A::word *ly,
@@ -460,12 +477,12 @@ __device__ __forceinline__ void fwd_all(const A &ar, typename A::word (&x)[16],
   constexpr bool last = g + 1 == Gr::G;
   fwd_group<A, LOGS, g, NPOLY, last ? SKIP : 0>(ar, x, y, tw, j, row, l1, zw);
   if constexpr (!last) {
-    exchange<LOGS, g, g + 1, NPOLY>(x, y, lx, ly, j);
-    fwd_all<A, LOGS, g + 1, NPOLY, SKIP>(ar, x, y, lx, ly, tw, j, row, l1, zw);
+    exchange<LOGS, g, g + 1, NPOLY, typename A::word, SYNC>(x, y, lx, ly, j);
+    fwd_all<A, LOGS, g + 1, NPOLY, SKIP, SYNC>(ar, x, y, lx, ly, tw, j, row, l1, zw);
   }
 }
 
-template <class A, int LOGS, int g, bool SCALE, int SKIP = 0>
+template <class A, int LOGS, int g, bool SCALE, int SKIP = 0, int SYNC = 0>
 __device__ __forceinline__ void inv_all(const KParams<A> &P, typename A::word (&x)[16],
                                         typename A::word (&y)[16], typename A::word *lx,
                                         typename A::word *ly,
@@ -474,8 +491,8 @@ __device__ __forceinline__ void inv_all(const KParams<A> &P, typename A::word (&
   using Gr = Groups<LOGS>;
   inv_group<A, LOGS, g, SCALE, g + 1 == Gr::G ? SKIP : 0>(P, x, tw, j, row, l1);
   if constexpr (g > 0) {
-    exchange<LOGS, g, g - 1, 1>(x, y, lx, ly, j);
-    inv_all<A, LOGS, g - 1, SCALE, SKIP>(P, x, y, lx, ly, tw, j, row, l1);
+    exchange<LOGS, g, g - 1, 1, typename A::word, SYNC>(x, y, lx, ly, j);
+    inv_all<A, LOGS, g - 1, SCALE, SKIP, SYNC>(P, x, y, lx, ly, tw, j, row, l1);
   }
 }
 
@@ -546,6 +563,21 @@ __host__ __device__ constexpr int rows_threads(int logs) {
 //   L1 == 0 : each unit is a whole polynomial (n = 2^LOGS): full product, canonical output.
 //   L1 >  0 : unit u is row (u mod 2^L1) of polynomial (u >> L1) after the column pass; the
 //             row's stages are global stages L1 .. L1+LOGS-1; output stays lazy in [0, 2q).
+#ifdef NTTMUL_WAVE_TRACE  // kbench instrumentation: per one-wave product, 100 MHz timestamps of
+                          // entry, inputs landed, transforms done, stores done (last launch wins)
+#if !defined(NTTMUL_KBENCH_BUILD)
+#error "NTTMUL_WAVE_TRACE is a tools/kbench instrumentation switch"
+#endif
+__device__ unsigned long long g_wave_trace[16384 * 4];
+hipError_t read_wave_trace(void *dst, size_t bytes) {
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_wave_trace), bytes);
+}
+#define WTRACE(k) \
+  do { if (LOGS == 10 && j == 0 && u < 16384) g_wave_trace[u * 4 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define WTRACE(k) do { } while (0)
+#endif
+
 template <class A, class TIn, class TOut, int LOGS, int L1>
 __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
     KParams<A> P, const TIn *__restrict__ a, const TIn *__restrict__ b, TOut *__restrict__ c,
@@ -570,6 +602,7 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
   const size_t base_r = base_l;
 #endif
 
+  WTRACE(0);
 #ifdef NTTMUL_STAGGER  // kbench experiment: one-wave blocks of generation blockIdx / 1024 wait
   if constexpr (LOGS == 10 && L1 == 0)
     for (unsigned i = 0; i < (blockIdx.x >> 10) * NTTMUL_STAGGER; i++) __builtin_amdgcn_s_sleep(8);
@@ -583,6 +616,9 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
                          sizeof(TIn) == 4 && sizeof(TOut) == 4;
   constexpr int kAux = NTTMUL_CPOL < 0 ? 0 : NTTMUL_CPOL;
   constexpr int kAuxSt = NTTMUL_CPOL_ST < 0 ? 0 : NTTMUL_CPOL_ST;
+  // n = 1024 one-wave products (C2: a single generation of waves that all wait for their loads):
+  // a's forward transform runs while b is still landing (NTTMUL_SPLIT_AB)
+  constexpr bool kSplitAB = NTTMUL_SPLIT_AB && kCpol && LOGS == 10;
 #if NTTMUL_ABL_NOLOAD
 #pragma unroll
   for (int k = 0; k < 16; k++) {
@@ -593,11 +629,18 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
   if constexpr (kCpol) {
     const size_t ub = live ? (size_t)blockIdx.x : 0;
     const auto ra = span_rsrc(a + ub * N, N), rb = span_rsrc(b + ub * N, N);
+    if constexpr (kSplitAB) {  // all of a first: a's transform starts before b has landed
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-      const int off = (Gr::base(0, j) + Gr::off(0, k)) * 4;
-      x[k] = (W)buf_ld32<kAux>(ra, off);
-      y[k] = (W)buf_ld32<kAux>(rb, off);
+      for (int k = 0; k < 16; k++) x[k] = (W)buf_ld32<kAux>(ra, (Gr::base(0, j) + Gr::off(0, k)) * 4);
+#pragma unroll
+      for (int k = 0; k < 16; k++) y[k] = (W)buf_ld32<kAux>(rb, (Gr::base(0, j) + Gr::off(0, k)) * 4);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        const int off = (Gr::base(0, j) + Gr::off(0, k)) * 4;
+        x[k] = (W)buf_ld32<kAux>(ra, off);
+        y[k] = (W)buf_ld32<kAux>(rb, off);
+      }
     }
   } else
 #endif
@@ -611,9 +654,19 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
   W *lx = lds[pb][0], *ly = lds[pb][lds_regions<W>() - 1];
   constexpr int D = NTTMUL_BASE_D ? A::kBaseD : 0;
   TwPair<W> zw[16];
-  fwd_all<A, LOGS, 0, 2, D>(P.ar, x, y, lx, ly, P.fw, j, row, L1, zw);
+#ifdef NTTMUL_WAVE_TRACE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  WTRACE(1);
+#endif
+  if constexpr (kSplitAB) {  // a's forward transform, then b's (each waits only for its loads)
+    fwd_all<A, LOGS, 0, 1, D>(P.ar, x, y, lx, ly, P.fw, j, row, L1, zw);
+    fwd_all<A, LOGS, 0, 1, D>(P.ar, y, x, lx, ly, P.fw, j, row, L1, zw);
+  } else {
+    fwd_all<A, LOGS, 0, 2, D>(P.ar, x, y, lx, ly, P.fw, j, row, L1, zw);
+  }
   base_mult<A, LOGS, D>(P.ar, x, y, zw);
   inv_all<A, LOGS, G - 1, L1 == 0, D>(P, x, y, lx, ly, P.iw, j, row, L1);
+  WTRACE(2);
 #if NTTMUL_ABL_NOSTORE
   W acc = 0;
 #pragma unroll
@@ -630,6 +683,10 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
         if (!A::kInvCanonical) v = P.ar.canon(v);
         buf_st32<kAuxSt>(rc, (Gr::base(0, j) + Gr::off(0, k)) * 4, (uint32_t)v);
       }
+#ifdef NTTMUL_WAVE_TRACE
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      WTRACE(3);
+#endif
     }
     return;
   }
@@ -642,6 +699,137 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
     }
   }
 }
+
+// C2 in-launch overlap experiments (tools/kbench builds only: both measured slower
+// than k_rows at C2 and at n = 1024 x 262144, profiles/r3/c2/)
+#ifdef NTTMUL_KBENCH_BUILD
+// Four independent one-wave products per 256-thread workgroup (n = 1024, u32 words): the k_rows
+// product with exchanges ordered per wave (xsync<1>) instead of per workgroup, so a quarter of
+// the workgroups to dispatch and no barrier coupling the four products.
+template <class A, int LOGS>
+__global__ __launch_bounds__(256) void k_rows_w4(KParams<A> P, const uint32_t *__restrict__ a,
+                                                 const uint32_t *__restrict__ b,
+                                                 uint32_t *__restrict__ c, size_t units) {
+  using W = typename A::word;
+  using Gr = Groups<LOGS>;
+  constexpr int N = Gr::N, NP = Gr::NP, G = Gr::G;
+  static_assert(N / 16 == 64, "one wave per product");
+  __shared__ W xch[4][NP];
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), j = threadIdx.x & 63;
+  const size_t u = (size_t)blockIdx.x * 4 + wv;
+  if (u >= units) return;
+  W *lx = xch[wv];
+  constexpr int kAux = NTTMUL_CPOL < 0 ? 0 : NTTMUL_CPOL;
+  constexpr int kAuxSt = NTTMUL_CPOL_ST < 0 ? 0 : NTTMUL_CPOL_ST;
+  W x[16], y[16];
+  const auto ra = span_rsrc(a + u * N, N), rb = span_rsrc(b + u * N, N);
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const int off = (Gr::base(0, j) + Gr::off(0, k)) * 4;
+    x[k] = (W)buf_ld32<kAux>(ra, off);
+    y[k] = (W)buf_ld32<kAux>(rb, off);
+  }
+  constexpr int D = NTTMUL_BASE_D ? A::kBaseD : 0;
+  TwPair<W> zw[16];
+  fwd_all<A, LOGS, 0, 2, D, 1>(P.ar, x, y, lx, lx, P.fw, j, 0, 0, zw);
+  base_mult<A, LOGS, D>(P.ar, x, y, zw);
+  inv_all<A, LOGS, G - 1, true, D, 1>(P, x, y, lx, lx, P.iw, j, 0, 0);
+  const auto rc = span_rsrc(c + u * N, N);
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    W v = x[k];
+    if (!A::kInvCanonical) v = P.ar.canon(v);
+    buf_st32<kAuxSt>(rc, (Gr::base(0, j) + Gr::off(0, k)) * 4, (uint32_t)v);
+  }
+}
+
+// Pipelined one-wave products (n = 1024, u32 words): a 256-thread workgroup of four independent
+// waves; each wave multiplies `per_wave` products in turn (units wave, wave + W, wave + 2W, ...,
+// W = 4 gridDim.x) and issues the loads of its next product before it transforms the current
+// one, so loads, arithmetic and stores of different products overlap inside one launch (a batch
+// of 4096 one-wave products is otherwise a single generation: every wave loads, then computes,
+// then stores, together).  The twiddles move to LDS once per workgroup (16 KiB), so a twiddle
+// read never waits behind the prefetch in the in-order vector-memory counter; exchanges are
+// ordered per wave (xsync<1>), so the four waves never wait for each other.
+template <class A, int LOGS>
+__global__ __launch_bounds__(256) void k_rows_pipe(KParams<A> P, const uint32_t *__restrict__ a,
+                                                   const uint32_t *__restrict__ b,
+                                                   uint32_t *__restrict__ c, size_t units) {
+  using W = typename A::word;
+  static_assert(sizeof(W) == 4, "u32 products");
+  using Gr = Groups<LOGS>;
+  constexpr int N = Gr::N, NP = Gr::NP, G = Gr::G;
+  static_assert(N / 16 == 64, "one wave per product");
+  __shared__ TwPair<W> tws[2 * N];
+  __shared__ W xch[4][NP];
+  {  // both twiddle tables into LDS: 2 N pairs of 8 B, 16 B per thread per step
+    const uint4 *fw4 = (const uint4 *)P.fw, *iw4 = (const uint4 *)P.iw;
+    uint4 *t4 = (uint4 *)tws;
+#pragma unroll
+    for (int i = threadIdx.x; i < N / 2; i += 256) {
+      t4[i] = fw4[i];
+      t4[N / 2 + i] = iw4[i];
+    }
+  }
+  __syncthreads();
+  // (readfirstlane: the wave index is wave-uniform, so the buffer descriptors are scalar)
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), j = threadIdx.x & 63;
+  const size_t stride = (size_t)gridDim.x * 4;
+  size_t u = (size_t)blockIdx.x * 4 + wv;
+  if (u >= units) return;
+  W *lx = xch[wv];
+  const TwPair<W> *fw = tws, *iw = tws + N;
+  constexpr int kAux = NTTMUL_CPOL < 0 ? 0 : NTTMUL_CPOL;
+  constexpr int kAuxSt = NTTMUL_CPOL_ST < 0 ? 0 : NTTMUL_CPOL_ST;
+  W x[16], y[16], nx[16], ny[16];
+  {
+    const auto ra = span_rsrc(a + u * N, N), rb = span_rsrc(b + u * N, N);
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const int off = (Gr::base(0, j) + Gr::off(0, k)) * 4;
+      x[k] = (W)buf_ld32<kAux>(ra, off);
+      y[k] = (W)buf_ld32<kAux>(rb, off);
+    }
+  }
+  constexpr int D = NTTMUL_BASE_D ? A::kBaseD : 0;
+  for (;;) {
+    const size_t un = u + stride;
+    const bool more = un < units;  // wave-uniform
+    {  // unconditional (the last product reloads itself), pinned ahead of the transforms
+      const size_t ul = more ? un : u;
+      const auto ra = span_rsrc(a + ul * N, N), rb = span_rsrc(b + ul * N, N);
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        const int off = (Gr::base(0, j) + Gr::off(0, k)) * 4;
+        nx[k] = (W)buf_ld32<kAux>(ra, off);
+        ny[k] = (W)buf_ld32<kAux>(rb, off);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    TwPair<W> zw[16];
+    fwd_all<A, LOGS, 0, 2, D, 1>(P.ar, x, y, lx, lx, fw, j, 0, 0, zw);
+    base_mult<A, LOGS, D>(P.ar, x, y, zw);
+    inv_all<A, LOGS, G - 1, true, D, 1>(P, x, y, lx, lx, iw, j, 0, 0);
+    {
+      const auto rc = span_rsrc(c + u * N, N);
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        W v = x[k];
+        if (!A::kInvCanonical) v = P.ar.canon(v);
+        buf_st32<kAuxSt>(rc, (Gr::base(0, j) + Gr::off(0, k)) * 4, (uint32_t)v);
+      }
+    }
+    if (!more) break;
+    u = un;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      x[k] = nx[k];
+      y[k] = ny[k];
+    }
+  }
+}
+
+#endif  // NTTMUL_KBENCH_BUILD
 
 // Standalone transforms, one polynomial per unit of 2^LOGS coefficients.
 //   DIR 0 (forward): NTT/ntt.C:342-371 mulntt_ct_std2rev — standard order in, bit-reversed out;
@@ -1085,11 +1273,47 @@ static hipError_t launch_rows(const KParams<A> &P, const void *a, const void *b,
   return hipGetLastError();
 }
 
+#ifdef NTTMUL_KBENCH_BUILD
+// Pipelined n = 1024 products (k_rows_pipe): T.pipe_per_wave products per wave (the grid
+// covers the batch with ceil(batch / (4 per_wave)) four-wave workgroups).
+template <class A>
+static hipError_t launch_pipe(const KParams<A> &P, const void *a, const void *b, void *c,
+                              size_t units, int per_wave, hipStream_t s) {
+  const size_t per_block = 4 * (size_t)per_wave;
+  const size_t blocks = (units + per_block - 1) / per_block;
+  if (tl_describe) {
+    describe_add(std::string("k_rows_pipe<") + AName<A>::v + ",10>");
+    return hipSuccess;
+  }
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL((k_rows_pipe<A, 10>), dim3((unsigned)blocks), dim3(256), 0, s, P,
+                     (const uint32_t *)a, (const uint32_t *)b, (uint32_t *)c, units);
+  return hipGetLastError();
+}
+#endif
+
 // Fused single-launch product, n = 2^logn <= 4096.
 template <class A, class IO>
 static hipError_t fused(const LaunchTables &T, const void *a, const void *b, void *c,
                         size_t batch, hipStream_t s) {
   const KParams<A> P = product_params<A>(T);
+#ifdef NTTMUL_KBENCH_BUILD
+  if constexpr (std::is_same<A, Arith32P>::value && std::is_same<IO, uint32_t>::value) {
+    if (T.logn == 10 && T.pipe_per_wave > 0)
+      return launch_pipe<A>(P, a, b, c, batch, T.pipe_per_wave, s);
+    if (T.logn == 10 && T.pipe_per_wave < 0) {  // k_rows_w4
+      if (tl_describe) {
+        describe_add(std::string("k_rows_w4<") + AName<A>::v + ",10>");
+        return hipSuccess;
+      }
+      const size_t blocks = (batch + 3) / 4;
+      if (blocks == 0) return hipSuccess;
+      hipLaunchKernelGGL((k_rows_w4<A, 10>), dim3((unsigned)blocks), dim3(256), 0, s, P,
+                         (const uint32_t *)a, (const uint32_t *)b, (uint32_t *)c, batch);
+      return hipGetLastError();
+    }
+  }
+#endif
   switch (T.logn) {
     case 8: return launch_rows<A, IO, IO, 8, 0>(P, a, b, c, batch, s);
     case 9: return launch_rows<A, IO, IO, 9, 0>(P, a, b, c, batch, s);

@@ -7,6 +7,11 @@
 
 #include "launch.hpp"
 #include "planner.hpp"
+#ifdef NTTMUL_WAVE_TRACE
+#include <algorithm>
+#include <vector>
+namespace nttmul { hipError_t read_wave_trace(void *dst, size_t bytes); }
+#endif
 
 #define CK(x)                                                                   \
   do {                                                                          \
@@ -44,6 +49,8 @@ int main(int argc, char **argv) {
   CK(hipDeviceGetAttribute(&T.cus, hipDeviceAttributeMultiprocessorCount, 0));
   // KB_MP_LAG > 0: n > 4096 products as one persistent launch (k_mp_persist) with this lag
   T.mp_lag = getenv("KB_MP_LAG") ? atoi(getenv("KB_MP_LAG")) : 0;
+  // KB_PIPE > 0: n = 1024 products through k_rows_pipe with KB_PIPE products per wave
+  T.pipe_per_wave = getenv("KB_PIPE") ? atoi(getenv("KB_PIPE")) : 0;
   if (T.mp_lag > 0 && P.logn > 12) CK(hipMemset(scr[3], 0, nttmul::mp_sync_bytes(batch)));
   unsigned long long *stats = nullptr;
 #if NTTMUL_MP_STATS
@@ -111,6 +118,23 @@ int main(int argc, char **argv) {
     for (size_t i = 0; i < cnt; i++) sum = sum * 1099511628211ull + h[i];
     free(h);
   }
+#ifdef NTTMUL_WAVE_TRACE
+  {  // phase percentiles of the last launch (us from the first wave's entry)
+    const size_t nw = batch < 16384 ? batch : 16384;
+    std::vector<unsigned long long> tr(nw * 4);
+    CK(nttmul::read_wave_trace(tr.data(), tr.size() * 8));
+    unsigned long long t0 = ~0ull;
+    for (size_t i = 0; i < nw; i++) t0 = std::min(t0, tr[i * 4]);
+    const char *nm[4] = {"entry", "loaded", "computed", "stored"};
+    for (int k = 0; k < 4; k++) {
+      std::vector<double> v(nw);
+      for (size_t i = 0; i < nw; i++) v[i] = (tr[i * 4 + k] - t0) * 0.01;
+      std::sort(v.begin(), v.end());
+      printf("  %-9s p0 %6.2f  p10 %6.2f  p50 %6.2f  p90 %6.2f  p100 %6.2f us\n", nm[k], v[0],
+             v[nw / 10], v[nw / 2], v[nw * 9 / 10], v[nw - 1]);
+    }
+  }
+#endif
   unsigned fault = 0;
   if (T.mp_lag > 0 && P.logn > 12) CK(hipMemcpy(&fault, (unsigned *)scr[3] + 1, 4, hipMemcpyDeviceToHost));
   if (fault) printf("FAULT: k_mp_persist poll gave up\n");
