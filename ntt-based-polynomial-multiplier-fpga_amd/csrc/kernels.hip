@@ -94,10 +94,16 @@
 #ifndef NTTMUL_ABL_NOSTORE
 #define NTTMUL_ABL_NOSTORE 0
 #endif
+// no "+ q" on the differences of a register group's last forward stage (wrong results: prices
+// the instruction a wave-uniform operand type across the exchange would save)
+#ifndef NTTMUL_ABL_BOUNDQ
+#define NTTMUL_ABL_BOUNDQ 0
+#endif
 // The ablation switches above give wrong products by design: they compile only into the
 // tools/kbench timing binaries (tools/kbench/build.sh passes NTTMUL_KBENCH_BUILD), never into
 // libnttmul.so
 #if (NTTMUL_ABL_TWMASK || NTTMUL_ABL_NOLOAD || NTTMUL_ABL_NOXCHG || NTTMUL_ABL_NOSTORE || \
+     NTTMUL_ABL_BOUNDQ || \
      NTTMUL_KBENCH_LITE || defined(NTTMUL_ABL_L2LOAD) || defined(NTTMUL_STAGGER)) && \
     !defined(NTTMUL_KBENCH_BUILD)
 #error "NTTMUL_ABL_* / NTTMUL_KBENCH_LITE are wrong-result kbench switches (tools/kbench/build.sh only)"
@@ -331,9 +337,10 @@ __device__ __forceinline__ void fwd_group(const A &ar, typename A::word (&x)[16]
         const bool xn = l > 0 && (k & (2 * dist));
         // (P_TYPED 2: the last stage before the base multiplication leaves its differences
         // signed as well; Arith32P::basemul corrects the -w blocks with the carry of x + q)
-        const bool yn = NTTMUL_P_TYPED >= 2
-                            ? l < S - SKIP - 1 || (SKIP > 0 && g + 1 == Gr::G)
-                            : l < S - SKIP - 1 && !((k + dist) & (dist >> 1));
+        const bool yn = NTTMUL_ABL_BOUNDQ ||
+                        (NTTMUL_P_TYPED >= 2
+                             ? l < S - SKIP - 1 || (SKIP > 0 && g + 1 == Gr::G)
+                             : l < S - SKIP - 1 && !((k + dist) & (dist >> 1)));
         const bool xc = NTTMUL_FIRST_XC && g == 0 && l == 0 && l1 == 0;
 #define NTTMUL_CT_P(XC_, XN_, YN_)                                         \
   do {                                                                     \

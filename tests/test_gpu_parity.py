@@ -282,6 +282,33 @@ def test_full_size_device_path(n, q, word_bits, batch, chunk_mb, lanes, lag, tor
     assert _check_whole_batch(n, q, word_bits, 0, batch, a, b, c) == batch
 
 
+@pytest.mark.parametrize("lag", MP_LAGS)
+def test_c5_bigint_golden(golden_dir, lag, torch_cuda, monkeypatch):
+    """C5 products (n = 65536, q = 0x3FFFFFFFFFE80001) on the device, through the product path the
+    bench runs (device-resident, counter-based inputs at their C5 batch positions) and as one
+    persistent launch: every output word's SHA-256 equals tests/golden/c5_bigint.json, computed by
+    Kronecker substitution with Python big integers -- no NTT, independent of the oracle."""
+    import hashlib
+    torch = torch_cuda
+    monkeypatch.setenv("NTTMUL_MP_LAG", str(lag))
+    g = json.load(open(os.path.join(golden_dir, "c5_bigint.json")))
+    n, q = g["n"], g["q"]
+    ctx = _ctx(n, q)
+    s = torch.cuda.current_stream().cuda_stream
+    for case in g["cases"]:
+        a = torch.empty(n, dtype=torch.int64, device="cuda")
+        b = torch.empty_like(a)
+        c = torch.empty_like(a)
+        ctx.fill_random_device(a, b, case["p0"], 1, 64, seed=g["seed"], stream=s)
+        if case["a"] == "all_q_minus_1":
+            a.fill_(q - 1)
+        ctx.multiply_device(c, a, b, 1, 64, stream=s)
+        torch.cuda.synchronize()
+        got = _as_np(c, 64)
+        assert hashlib.sha256(got.astype("<u8").tobytes()).hexdigest() == case["sha256"], case
+        assert [int(x) for x in got[:8]] == case["head"] and int(got[-1]) == case["last"]
+
+
 def test_c4_last_rank_slice(torch_cuda):
     """C4 (n = 4096, 2^20 products over 8 GPUs): the slice rank 7 owns, at its full size
     (131,072 products from global index 7 * 131,072), generated and multiplied on this device as

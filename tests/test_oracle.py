@@ -232,3 +232,22 @@ def test_reference_anchors_run_and_agree():
     r = O.ref_anchors(reps256=50, reps1024=10)
     assert len(r) == 6, r
     assert all(0 < v < 1e-2 for v in r.values())
+
+
+def test_c5_oracle_vs_bigint_golden(golden_dir):
+    """C5 size (n = 65536, 62-bit q): the oracle's restated P4 product equals the golden digests
+    of tests/golden/c5_bigint.json, which were computed by Kronecker substitution with Python big
+    integers (no NTT anywhere; tests/golden/make_c5_bigint.py) -- an independent pin of the
+    restatement at the size the reference cannot run."""
+    import hashlib
+    import json
+    g = json.load(open(os.path.join(golden_dir, "c5_bigint.json")))
+    n, q = g["n"], g["q"]
+    P = O.Plan(n, q)
+    for case in g["cases"]:
+        a, b = O.fill_inputs(n, q, case["p0"], 1, g["seed"])
+        if case["a"] == "all_q_minus_1":
+            a[0][:] = q - 1
+        c = P.product_batch(a, b)[0].reshape(n)
+        assert hashlib.sha256(c.astype("<u8").tobytes()).hexdigest() == case["sha256"], case["p0"]
+        assert [int(x) for x in c[:8]] == case["head"] and int(c[-1]) == case["last"]
