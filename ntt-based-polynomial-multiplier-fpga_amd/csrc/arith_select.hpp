@@ -48,6 +48,14 @@ constexpr int groups_g(int logs) { return (logs + 3) / 4; }
 constexpr int groups_s(int logs, int g) {
   return logs / groups_g(logs) + (g < logs % groups_g(logs) ? 1 : 0);
 }
+// Wave-typed register-group layouts of the Plantard kernels' 4096-coefficient rows (kernels.hip
+// Groups WT); planner and kernels must agree.  Off: C3 +2.0 % time (1.034 vs 1.013 ms, kbench
+// A/B, identical checksums, profiles/r3/c3/wave_typed_ab.txt) -- the permuted layouts' address
+// math and the branch's join copies cost more than the 32 boundary instructions they remove
+#ifndef NTTMUL_WAVE_TYPED
+#define NTTMUL_WAVE_TYPED 0
+#endif
+constexpr bool wave_typed_rows(int logs) { return NTTMUL_WAVE_TYPED && logs == 12; }
 // Arith32P, NTTMUL_P_TYPED == 2: forward twiddle entry idx = 2^st + j serves stage st; at a
 // stage that is not the first of its register group, the multiplicand of the butterflies using
 // an odd entry is the previous stage's difference (bit 2d of the element = the entry's low bit),
@@ -60,7 +68,10 @@ constexpr bool p_signed_fw_entry(int logn, uint32_t idx) {
   if (local < 0) return false;  // column pass: unsigned operands
   int g = 0, st0 = 0;
   while (st0 + groups_s(logs, g) <= local) st0 += groups_s(logs, g++);
-  return local - st0 >= 1 && (idx & 1);
+  // wave-typed layouts (kernels.hip Groups WT, 4096-coefficient rows): the first stage of groups
+  // 1 and 2 multiplies the previous group's differences, left signed across the exchange, by the
+  // odd entries as well
+  return (local - st0 >= 1 || (wave_typed_rows(logs) && g >= 1)) && (idx & 1);
 }
 
 // Arith32P3 (base blocks of 8 coefficients, n = 4096 products only): each output sums eight

@@ -137,8 +137,20 @@ static void describe_add(const std::string &k) {
 // ---------------------------------------------------------------------------------------------
 // Layout algebra of the register groups (all compile-time except the per-thread base)
 // ---------------------------------------------------------------------------------------------
-template <int LOGS>
+// WT (wave-typed layouts, n = 4096 rows of the Plantard kernels, NTTMUL_WAVE_TYPED): groups 1
+// and 2 take their element bits from the thread index in another order, so that the bit that
+// says whether the previous group's last forward stage wrote an element as a sum or as a
+// difference (element bit 8 after group 0, bit 4 after group 1) is thread bit 6 -- the same for
+// a whole wave.  Those last stages can then leave their differences signed across the LDS
+// exchange (one instruction less per butterfly, -0.85 % time by ablation, profiles/r3/c3/) and
+// the next group's first stage picks its operand type with one wave-uniform branch.  Group 1:
+// thread bits 0-3 -> element bits 0-3, 4 -> 9, 5 -> 10, 6 -> 8, 7 -> 11; group 2: thread bits
+// 0-5 -> element bits 5-10, 6 -> 4, 7 -> 11.  Both exchanges then pad e + (e >> 5), which the bank
+// census (tests/test_layout.py) finds conflict-free for both layouts of each exchange.
+// (NTTMUL_WAVE_TYPED: arith_select.hpp, shared with the planner's twiddle forms)
+template <int LOGS, bool WT = false>
 struct Groups {
+  static_assert(!WT || LOGS == 12, "wave-typed layouts are defined for 4096-coefficient rows");
   static constexpr int N = 1 << LOGS;
   static constexpr int G = (LOGS + 3) / 4;
   static constexpr int S(int g) { return LOGS / G + (g < LOGS % G ? 1 : 0); }
@@ -158,7 +170,18 @@ struct Groups {
     if (lr >= LNS(g)) return sidx + (m << lr);
     return ((sidx >> lr) << (lr + s)) + (sidx & ((1 << lr) - 1)) + (m << lr);
   }
+  __host__ __device__ static constexpr int base_wt(int g, int j) {
+    return g == 1 ? (j & 15) + (((j >> 4) & 1) << 9) + (((j >> 5) & 1) << 10) +
+                        (((j >> 6) & 1) << 8) + (((j >> 7) & 1) << 11)
+                  : ((j & 63) << 5) + (((j >> 6) & 1) << 4) + (((j >> 7) & 1) << 11);
+  }
+  // WT: the operand type (0 sum, 1 difference) of the elements a thread holds at the start of
+  // register group g >= 1; thread bit 6, uniform over the wave
+  __device__ static __forceinline__ int wave_type(int j) {
+    return __builtin_amdgcn_readfirstlane((j >> 6) & 1);
+  }
   __device__ static __forceinline__ int base(int g, int j) {
+    if (WT && g > 0) return base_wt(g, j);
     int lr = LR(g), s = S(g), lns = LNS(g);
     if (lr >= lns) {
       int set0 = j << lns;
@@ -171,6 +194,7 @@ struct Groups {
     int lr = LR(g), lns = LNS(g);
     int sidx = k % NS(g);
     if (g == 0) return 0;
+    if (WT) return base_wt(g, j) >> (lr + S(g));  // the element bits above the group's stages
     if (lr >= lns) return (j << lns) >> lr;
     return (j << (lns - lr)) + (sidx >> lr);
   }
@@ -193,12 +217,14 @@ struct Groups {
   static constexpr bool kPad0 = NTTMUL_PAD0 && LOGS >= 10 && G > 2;
   static constexpr bool kPad2 = NTTMUL_PAD0 && NTTMUL_PAD2 && (LOGS == 10 || LOGS == 9);
   static constexpr int PS(int x) {
-    return kPad2 ? (LOGS == 10 ? (x == 0 ? 6 : 4) : (x == 0 ? 5 : 4))
-                 : (x == 0 && kPad0 ? LOGS - 4 : 4);
+    return WT ? 5
+              : kPad2 ? (LOGS == 10 ? (x == 0 ? 6 : 4) : (x == 0 ? 5 : 4))
+                      : (x == 0 && kPad0 ? LOGS - 4 : 4);
   }
   static constexpr int PT(int x) {
-    return kPad2 ? (LOGS == 10 ? (x == 0 ? 3 : 1) : (x == 0 ? 0 : 1))
-                 : (x == 0 && kPad0 ? LOGS - 8 : 0);
+    return WT ? 0
+              : kPad2 ? (LOGS == 10 ? (x == 0 ? 3 : 1) : (x == 0 ? 0 : 1))
+                      : (x == 0 && kPad0 ? LOGS - 8 : 0);
   }
   static constexpr int PS2(int x) { return kPad2 ? (LOGS == 10 ? 8 : (x == 0 ? 7 : 8)) : 31; }
   template <int X>
@@ -242,6 +268,12 @@ __host__ __device__ constexpr bool kTypedP() {
   if constexpr (IsPlantard<A>::value) return A::kTypedP;
   return false;
 }
+// wave-typed layouts (Groups WT) for the typed Plantard kernels' 4096-coefficient rows; the
+// planner stores the matching twiddle forms (arith_select.hpp p_signed_fw_entry)
+template <class A, int LOGS>
+__host__ __device__ constexpr bool kWT() {
+  return wave_typed_rows(LOGS) && kTypedP<A>() && NTTMUL_P_TYPED >= 2;
+}
 
 // Coefficient streams are touched once per product: NTTMUL_NT marks them non-temporal.  The row
 // pass of a multi-pass product (L1 > 0) reads and writes intermediates that the column passes
@@ -284,88 +316,115 @@ __device__ __forceinline__ void buf_st32(R r, int byte_off, uint32_t v) {
   __builtin_amdgcn_raw_buffer_store_b32(v, r, byte_off, 0, AUX);
 }
 
+// One forward CT stage l of group g on NPOLY (1 or 2) polynomials (same twiddles); the twiddles
+// of the group's last performed stage are kept in zw[X register] (see base_mult).  TIN: under the
+// wave-typed layouts (kWT) the operand type of the first stage of groups g >= 1, chosen by the
+// caller's wave-uniform branch (1: the previous group's differences, left signed).
+template <class A, int LOGS, int g, int NPOLY, int SKIP, int TIN>
+__device__ __forceinline__ void fwd_stage(const A &ar, typename A::word (&x)[16],
+                                          typename A::word (&y)[16],
+                                          const TwPair<typename A::word> *__restrict__ tw, int j,
+                                          int row, int l1, TwPair<typename A::word> (&zw)[16],
+                                          int l) {
+  using Gr = Groups<LOGS, kWT<A, LOGS>()>;
+  constexpr int S = Gr::S(g), st0 = Gr::ST0(g), ns = Gr::NS(g);
+  const int dist = 8 >> l;
+  const int st = st0 + l;
+  const int tbase = (1 << (l1 + st)) + (row << st);
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    if (k & dist) continue;
+    const int m = k / ns;
+    const int idx = tbase + (Gr::blk(g, j, k) << l) + (m >> (S - l));
+    if constexpr (A::kTyped) {
+      // operand type: bit 2 dist of k says the previous stage of this group wrote it as Y
+      // (N-type); the group's first stage reads P-type; its last writes P-type
+      const bool in_n = l > 0 && (k & (2 * dist));
+      const bool out_p = l == S - SKIP - 1;
+      const TwPair<typename A::word> t = in_n ? tw[idx + (1 << (l1 + LOGS))] : tw[idx];
+      if (out_p) zw[k] = t;
+      const bool xc = NTTMUL_FIRST_XC && g == 0 && l == 0 && l1 == 0;
+#define NTTMUL_CT_T(IN, OUT, XC_)                                 \
+  do {                                                            \
+    ar.template ct_t<IN, OUT, XC_>(x[k], x[k + dist], t.w, t.ws); \
+    if (NPOLY == 2) ar.template ct_t<IN, OUT, XC_>(y[k], y[k + dist], t.w, t.ws); \
+  } while (0)
+      if (xc) {
+        if (out_p) NTTMUL_CT_T(false, true, true); else NTTMUL_CT_T(false, false, true);
+      } else if (in_n) {
+        if (out_p) NTTMUL_CT_T(true, true, false); else NTTMUL_CT_T(true, false, false);
+      } else {
+        if (out_p) NTTMUL_CT_T(false, true, false); else NTTMUL_CT_T(false, false, false);
+      }
+#undef NTTMUL_CT_T
+      continue;
+    }
+    const TwPair<typename A::word> t = tw[NTTMUL_ABL_TWMASK ? (idx & NTTMUL_ABL_TWMASK) : idx];
+    if (l == S - SKIP - 1) zw[k] = t;
+    if constexpr (kTypedP<A>()) {
+      // Arith32P: register k was written as a (signed) difference by the previous stage iff
+      // bit 2 dist is set; this stage leaves its difference in k + dist signed iff the next
+      // stage of the group uses that register as an X (bit dist / 2 clear).  kWT: the first
+      // stage of groups 1 and 2 reads the type TIN of the wave
+      constexpr bool kWt = kWT<A, LOGS>();
+      const bool xn = l > 0 ? (k & (2 * dist)) != 0 : (kWt && g > 0 && TIN);
+      // (P_TYPED 2: the last stage before the base multiplication leaves its differences
+      // signed as well; Arith32P::basemul corrects the -w blocks with the carry of x + q; kWT:
+      // so does the last stage before an exchange)
+      const bool yn = NTTMUL_ABL_BOUNDQ ||
+                      (NTTMUL_P_TYPED >= 2
+                           ? l < S - SKIP - 1 || (SKIP > 0 && g + 1 == Gr::G) ||
+                                 (kWt && g + 1 < Gr::G)
+                           : l < S - SKIP - 1 && !((k + dist) & (dist >> 1)));
+      const bool xc = NTTMUL_FIRST_XC && g == 0 && l == 0 && l1 == 0;
+      constexpr bool kAsm = kWt && g > 0 && TIN;  // see Arith32P::pmul_s
+#define NTTMUL_CT_P(XC_, XN_, YN_)                                         \
+  do {                                                                     \
+    ar.template ct<XC_, XN_, YN_, kAsm>(x[k], x[k + dist], t.w, t.ws);      \
+    if (NPOLY == 2) ar.template ct<XC_, XN_, YN_, kAsm>(y[k], y[k + dist], t.w, t.ws); \
+  } while (0)
+      if (xc) {
+        if (yn) NTTMUL_CT_P(true, false, true); else NTTMUL_CT_P(true, false, false);
+      } else if (xn) {
+        if (yn) NTTMUL_CT_P(false, true, true); else NTTMUL_CT_P(false, true, false);
+      } else {
+        if (yn) NTTMUL_CT_P(false, false, true); else NTTMUL_CT_P(false, false, false);
+      }
+#undef NTTMUL_CT_P
+      continue;
+    }
+    // global stage 0 of a whole polynomial reads canonical input (the API contract, [0, q)):
+    // its X operands need no reduction
+    if (NTTMUL_FIRST_XC && g == 0 && l == 0 && l1 == 0) {
+      ar.template ct<true>(x[k], x[k + dist], t.w, t.ws);
+      if (NPOLY == 2) ar.template ct<true>(y[k], y[k + dist], t.w, t.ws);
+    } else {
+      ar.ct(x[k], x[k + dist], t.w, t.ws);
+      if (NPOLY == 2) ar.ct(y[k], y[k + dist], t.w, t.ws);
+    }
+  }
+}
+
 // Forward CT stages of group g on NPOLY (1 or 2) polynomials (same twiddles).  SKIP: leave out
 // the last SKIP stages of the group (the incomplete transform of the product kernel, see
-// base_mult); the twiddles of the last stage performed are kept in zw[X register].
+// base_mult).
 template <class A, int LOGS, int g, int NPOLY = 2, int SKIP = 0>
 __device__ __forceinline__ void fwd_group(const A &ar, typename A::word (&x)[16],
                                           typename A::word (&y)[16],
                                           const TwPair<typename A::word> *__restrict__ tw, int j,
                                           int row, int l1,
                                           TwPair<typename A::word> (&zw)[16]) {
-  using Gr = Groups<LOGS>;
-  constexpr int S = Gr::S(g), st0 = Gr::ST0(g), ns = Gr::NS(g);
+  using Gr = Groups<LOGS, kWT<A, LOGS>()>;
+  constexpr int S = Gr::S(g);
 #pragma unroll
   for (int l = 0; l < S - SKIP; l++) {
-    const int dist = 8 >> l;
-    const int st = st0 + l;
-    const int tbase = (1 << (l1 + st)) + (row << st);
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-      if (k & dist) continue;
-      const int m = k / ns;
-      const int idx = tbase + (Gr::blk(g, j, k) << l) + (m >> (S - l));
-      if constexpr (A::kTyped) {
-        // operand type: bit 2 dist of k says the previous stage of this group wrote it as Y
-        // (N-type); the group's first stage reads P-type; its last writes P-type
-        const bool in_n = l > 0 && (k & (2 * dist));
-        const bool out_p = l == S - SKIP - 1;
-        const TwPair<typename A::word> t = in_n ? tw[idx + (1 << (l1 + LOGS))] : tw[idx];
-        if (out_p) zw[k] = t;
-        const bool xc = NTTMUL_FIRST_XC && g == 0 && l == 0 && l1 == 0;
-#define NTTMUL_CT_T(IN, OUT, XC_)                                 \
-  do {                                                            \
-    ar.template ct_t<IN, OUT, XC_>(x[k], x[k + dist], t.w, t.ws); \
-    if (NPOLY == 2) ar.template ct_t<IN, OUT, XC_>(y[k], y[k + dist], t.w, t.ws); \
-  } while (0)
-        if (xc) {
-          if (out_p) NTTMUL_CT_T(false, true, true); else NTTMUL_CT_T(false, false, true);
-        } else if (in_n) {
-          if (out_p) NTTMUL_CT_T(true, true, false); else NTTMUL_CT_T(true, false, false);
-        } else {
-          if (out_p) NTTMUL_CT_T(false, true, false); else NTTMUL_CT_T(false, false, false);
-        }
-#undef NTTMUL_CT_T
-        continue;
-      }
-      const TwPair<typename A::word> t = tw[NTTMUL_ABL_TWMASK ? (idx & NTTMUL_ABL_TWMASK) : idx];
-      if (l == S - SKIP - 1) zw[k] = t;
-      if constexpr (kTypedP<A>()) {
-        // Arith32P: register k was written as a (signed) difference by the previous stage iff
-        // bit 2 dist is set; this stage leaves its difference in k + dist signed iff the next
-        // stage of the group uses that register as an X (bit dist / 2 clear)
-        const bool xn = l > 0 && (k & (2 * dist));
-        // (P_TYPED 2: the last stage before the base multiplication leaves its differences
-        // signed as well; Arith32P::basemul corrects the -w blocks with the carry of x + q)
-        const bool yn = NTTMUL_ABL_BOUNDQ ||
-                        (NTTMUL_P_TYPED >= 2
-                             ? l < S - SKIP - 1 || (SKIP > 0 && g + 1 == Gr::G)
-                             : l < S - SKIP - 1 && !((k + dist) & (dist >> 1)));
-        const bool xc = NTTMUL_FIRST_XC && g == 0 && l == 0 && l1 == 0;
-#define NTTMUL_CT_P(XC_, XN_, YN_)                                         \
-  do {                                                                     \
-    ar.template ct<XC_, XN_, YN_>(x[k], x[k + dist], t.w, t.ws);            \
-    if (NPOLY == 2) ar.template ct<XC_, XN_, YN_>(y[k], y[k + dist], t.w, t.ws); \
-  } while (0)
-        if (xc) {
-          if (yn) NTTMUL_CT_P(true, false, true); else NTTMUL_CT_P(true, false, false);
-        } else if (xn) {
-          if (yn) NTTMUL_CT_P(false, true, true); else NTTMUL_CT_P(false, true, false);
-        } else {
-          if (yn) NTTMUL_CT_P(false, false, true); else NTTMUL_CT_P(false, false, false);
-        }
-#undef NTTMUL_CT_P
-        continue;
-      }
-      // global stage 0 of a whole polynomial reads canonical input (the API contract, [0, q)):
-      // its X operands need no reduction
-      if (NTTMUL_FIRST_XC && g == 0 && l == 0 && l1 == 0) {
-        ar.template ct<true>(x[k], x[k + dist], t.w, t.ws);
-        if (NPOLY == 2) ar.template ct<true>(y[k], y[k + dist], t.w, t.ws);
-      } else {
-        ar.ct(x[k], x[k + dist], t.w, t.ws);
-        if (NPOLY == 2) ar.ct(y[k], y[k + dist], t.w, t.ws);
-      }
+    if (kWT<A, LOGS>() && g > 0 && l == 0) {  // one wave-uniform branch per group
+      if (Gr::wave_type(j))
+        fwd_stage<A, LOGS, g, NPOLY, SKIP, 1>(ar, x, y, tw, j, row, l1, zw, l);
+      else
+        fwd_stage<A, LOGS, g, NPOLY, SKIP, 0>(ar, x, y, tw, j, row, l1, zw, l);
+    } else {
+      fwd_stage<A, LOGS, g, NPOLY, SKIP, 0>(ar, x, y, tw, j, row, l1, zw, l);
     }
   }
 }
@@ -376,7 +435,7 @@ template <class A, int LOGS, int g, bool SCALE, int SKIP = 0>
 __device__ __forceinline__ void inv_group(const KParams<A> &P, typename A::word (&x)[16],
                                           const TwPair<typename A::word> *__restrict__ tw, int j,
                                           int row, int l1) {
-  using Gr = Groups<LOGS>;
+  using Gr = Groups<LOGS, kWT<A, LOGS>()>;
   constexpr int S = Gr::S(g), st0 = Gr::ST0(g), ns = Gr::NS(g);
 #pragma unroll
   for (int l = S - 1 - SKIP; l >= 0; l--) {
@@ -436,9 +495,9 @@ __device__ __forceinline__ void xsync() {
 }
 
 // Move 16 registers of each region from layout gfrom to layout gto through LDS.
-template <int LOGS, int gfrom, int gto, int NREG, class W, int SYNC = 0>
+template <int LOGS, int gfrom, int gto, int NREG, class W, int SYNC = 0, bool WT = false>
 __device__ __forceinline__ void exchange(W (&x)[16], W (&y)[16], W *lds_x, W *lds_y, int j) {
-  using Gr = Groups<LOGS>;
+  using Gr = Groups<LOGS, WT>;
 #if NTTMUL_ABL_NOXCHG
   return;
 #endif
@@ -480,11 +539,11 @@ __device__ __forceinline__ void fwd_all(const A &ar, typename A::word (&x)[16],
                                         typename A::word *ly,
                                         const TwPair<typename A::word> *__restrict__ tw, int j,
                                         int row, int l1, TwPair<typename A::word> (&zw)[16]) {
-  using Gr = Groups<LOGS>;
+  using Gr = Groups<LOGS, kWT<A, LOGS>()>;
   constexpr bool last = g + 1 == Gr::G;
   fwd_group<A, LOGS, g, NPOLY, last ? SKIP : 0>(ar, x, y, tw, j, row, l1, zw);
   if constexpr (!last) {
-    exchange<LOGS, g, g + 1, NPOLY, typename A::word, SYNC>(x, y, lx, ly, j);
+    exchange<LOGS, g, g + 1, NPOLY, typename A::word, SYNC, kWT<A, LOGS>()>(x, y, lx, ly, j);
     fwd_all<A, LOGS, g + 1, NPOLY, SKIP, SYNC>(ar, x, y, lx, ly, tw, j, row, l1, zw);
   }
 }
@@ -495,10 +554,10 @@ __device__ __forceinline__ void inv_all(const KParams<A> &P, typename A::word (&
                                         typename A::word *ly,
                                         const TwPair<typename A::word> *__restrict__ tw, int j,
                                         int row, int l1) {
-  using Gr = Groups<LOGS>;
+  using Gr = Groups<LOGS, kWT<A, LOGS>()>;
   inv_group<A, LOGS, g, SCALE, g + 1 == Gr::G ? SKIP : 0>(P, x, tw, j, row, l1);
   if constexpr (g > 0) {
-    exchange<LOGS, g, g - 1, 1, typename A::word, SYNC>(x, y, lx, ly, j);
+    exchange<LOGS, g, g - 1, 1, typename A::word, SYNC, kWT<A, LOGS>()>(x, y, lx, ly, j);
     inv_all<A, LOGS, g - 1, SCALE, SKIP, SYNC>(P, x, y, lx, ly, tw, j, row, l1);
   }
 }
@@ -513,8 +572,8 @@ __device__ __forceinline__ void inv_all(const KParams<A> &P, typename A::word (&
 template <class A, int LOGS, int D>
 __device__ __forceinline__ void base_mult(const A &ar, typename A::word (&x)[16],
                                           const typename A::word (&y)[16],
-                                          const TwPair<typename A::word> (&zw)[16]) {
-  using Gr = Groups<LOGS>;
+                                          const TwPair<typename A::word> (&zw)[16], int j) {
+  using Gr = Groups<LOGS, kWT<A, LOGS>()>;
   constexpr int g = Gr::G - 1, B = 1 << D;
   static_assert(D == 0 || Gr::S(g) > D, "last register group too short for the base blocks");
   if constexpr (D == 0) {
@@ -530,13 +589,21 @@ __device__ __forceinline__ void base_mult(const A &ar, typename A::word (&x)[16]
       for (int i = 0; i < B; i++) r[i] = Gr::reg_of(g, o0 + i);
       const bool neg = (o0 >> D) & 1;
       const int kz = Gr::reg_of(g, o0 & ~B);
-      const TwPair<typename A::word> z = zw[kz];
+      TwPair<typename A::word> z = zw[kz];
       // typed arithmetic: the last forward stage (dist 8 >> (S - D - 1)) multiplied N-type
       // operands, and so kept the centred twiddle, when bit 2 dist of its X register is set
       constexpr int dl = 8 >> (Gr::S(g) - D - 1);
       // (Arith32P, NTTMUL_P_TYPED 2: the same condition says the pair is in signed form)
       constexpr bool typed_z = A::kTyped || (kTypedP<A>() && NTTMUL_P_TYPED >= 2);
-      const bool zc = typed_z && Gr::S(g) - D - 1 > 0 && (kz & (2 * dl));
+      // (kWT, when that stage was its group's first: the pair is in signed form exactly when the
+      // wave's elements were the previous group's differences.  The signed-input product is
+      // exact for canonical inputs too, so every wave takes it: the unsigned pair of the other
+      // waves becomes the signed one by b1 + (b0 >> 31), two instructions, instead of a second
+      // copy of the base multiplication behind a branch)
+      constexpr bool kWtFirst = kWT<A, LOGS>() && Gr::S(g) - D - 1 == 0;
+      if constexpr (kWtFirst)
+        z.ws += (typename A::word)((z.w >> 31) & (1 - Gr::wave_type(j)));
+      const bool zc = typed_z && (kWtFirst || (Gr::S(g) - D - 1 > 0 && (kz & (2 * dl))));
       typename A::word a[B], b[B];
 #pragma unroll
       for (int i = 0; i < B; i++) a[i] = x[r[i]], b[i] = y[r[i]];
@@ -590,7 +657,7 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
     KParams<A> P, const TIn *__restrict__ a, const TIn *__restrict__ b, TOut *__restrict__ c,
     size_t units) {
   using W = typename A::word;
-  using Gr = Groups<LOGS>;
+  using Gr = Groups<LOGS, kWT<A, LOGS>()>;
   constexpr int N = Gr::N, TP = N / 16, PB = rows_threads(LOGS) / TP, G = Gr::G, NP = Gr::NP;
   constexpr bool kNT = NTTMUL_NT && (L1 == 0 || NTTMUL_NT_MP);
   __shared__ W lds[PB][lds_regions<W>()][NP];
@@ -671,7 +738,7 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
   } else {
     fwd_all<A, LOGS, 0, 2, D>(P.ar, x, y, lx, ly, P.fw, j, row, L1, zw);
   }
-  base_mult<A, LOGS, D>(P.ar, x, y, zw);
+  base_mult<A, LOGS, D>(P.ar, x, y, zw, j);
   inv_all<A, LOGS, G - 1, L1 == 0, D>(P, x, y, lx, ly, P.iw, j, row, L1);
   WTRACE(2);
 #if NTTMUL_ABL_NOSTORE
@@ -718,7 +785,7 @@ __global__ __launch_bounds__(256) void k_rows_w4(KParams<A> P, const uint32_t *_
                                                  const uint32_t *__restrict__ b,
                                                  uint32_t *__restrict__ c, size_t units) {
   using W = typename A::word;
-  using Gr = Groups<LOGS>;
+  using Gr = Groups<LOGS, kWT<A, LOGS>()>;
   constexpr int N = Gr::N, NP = Gr::NP, G = Gr::G;
   static_assert(N / 16 == 64, "one wave per product");
   __shared__ W xch[4][NP];
@@ -739,7 +806,7 @@ __global__ __launch_bounds__(256) void k_rows_w4(KParams<A> P, const uint32_t *_
   constexpr int D = NTTMUL_BASE_D ? A::kBaseD : 0;
   TwPair<W> zw[16];
   fwd_all<A, LOGS, 0, 2, D, 1>(P.ar, x, y, lx, lx, P.fw, j, 0, 0, zw);
-  base_mult<A, LOGS, D>(P.ar, x, y, zw);
+  base_mult<A, LOGS, D>(P.ar, x, y, zw, j);
   inv_all<A, LOGS, G - 1, true, D, 1>(P, x, y, lx, lx, P.iw, j, 0, 0);
   const auto rc = span_rsrc(c + u * N, N);
 #pragma unroll
@@ -764,7 +831,7 @@ __global__ __launch_bounds__(256) void k_rows_pipe(KParams<A> P, const uint32_t 
                                                    uint32_t *__restrict__ c, size_t units) {
   using W = typename A::word;
   static_assert(sizeof(W) == 4, "u32 products");
-  using Gr = Groups<LOGS>;
+  using Gr = Groups<LOGS, kWT<A, LOGS>()>;
   constexpr int N = Gr::N, NP = Gr::NP, G = Gr::G;
   static_assert(N / 16 == 64, "one wave per product");
   __shared__ TwPair<W> tws[2 * N];
@@ -815,7 +882,7 @@ __global__ __launch_bounds__(256) void k_rows_pipe(KParams<A> P, const uint32_t 
     }
     TwPair<W> zw[16];
     fwd_all<A, LOGS, 0, 2, D, 1>(P.ar, x, y, lx, lx, fw, j, 0, 0, zw);
-    base_mult<A, LOGS, D>(P.ar, x, y, zw);
+    base_mult<A, LOGS, D>(P.ar, x, y, zw, j);
     inv_all<A, LOGS, G - 1, true, D, 1>(P, x, y, lx, lx, iw, j, 0, 0);
     {
       const auto rc = span_rsrc(c + u * N, N);
@@ -849,7 +916,7 @@ template <class A, class TIn, class TOut, int LOGS, int L1, int DIR>
 __global__ __launch_bounds__(256) void k_xform(KParams<A> P, const TIn *__restrict__ in,
                                                TOut *__restrict__ out, size_t units) {
   using W = typename A::word;
-  using Gr = Groups<LOGS>;
+  using Gr = Groups<LOGS, kWT<A, LOGS>()>;
   constexpr int N = Gr::N, TP = N / 16, PB = 256 / TP, G = Gr::G, NP = Gr::NP;
   constexpr int GIN = DIR == 0 ? 0 : G - 1, GOUT = DIR == 0 ? G - 1 : 0;
   __shared__ W lds[PB][NP];
@@ -1066,7 +1133,7 @@ __global__ __launch_bounds__(256) void k_mp_persist(KParams<A> P, const IO *__re
                                                     unsigned batch, MpSync S) {
   using W = typename A::word;
   constexpr int LOGS = 12, NR = 1 << L1, M = 1 << L1;
-  using Gr = Groups<LOGS>;
+  using Gr = Groups<LOGS, kWT<A, LOGS>()>;
   constexpr int N = Gr::N, G = Gr::G, NP = Gr::NP;
   constexpr unsigned T = 2 * kMpCols + NR;
   constexpr size_t kPoly = (size_t)N << L1;   // words per polynomial
@@ -1133,7 +1200,7 @@ __global__ __launch_bounds__(256) void k_mp_persist(KParams<A> P, const IO *__re
         constexpr int D = NTTMUL_BASE_D ? A::kBaseD : 0;
         TwPair<W> zw[16];
         fwd_all<A, LOGS, 0, 2, D>(P.ar, x, y, lds, lds, P.fw, j, row, L1, zw);
-        base_mult<A, LOGS, D>(P.ar, x, y, zw);
+        base_mult<A, LOGS, D>(P.ar, x, y, zw, j);
         inv_all<A, LOGS, G - 1, false, D>(P, x, y, lds, lds, P.iw, j, row, L1);
 #pragma unroll
         for (int q = 0; q < 16; q++) st_pol<NTTMUL_MP_POL>(tc + base + Gr::off(0, q), x[q]);

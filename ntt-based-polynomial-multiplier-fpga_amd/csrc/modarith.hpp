@@ -347,8 +347,17 @@ struct Arith32P {
   // signed pair (b0, b1 + (b0 >> 31)) of the planner: T = x BR mod 2^64 through v_mul_hi_i32, and
   // t = floor((T_hi q + A) / 2^32) is exact for A in [q + 2^31 q / 2^32, 2^32 - 2^31 q / 2^32),
   // non-empty for q < 2^31 (the error term spans 2^32 q < 2^32 (2^32 - q)); A = ceil(1.5 q)
+  // ASM: the signed high product as opaque inline asm -- for a stage compiled twice behind a
+  // wave-uniform branch (kernels.hip fwd_stage, TIN), where the optimizer would otherwise merge
+  // the two copies' high products into one 64-bit multiply with selects
+  template <bool ASM = false>
   __device__ __forceinline__ uint32_t pmul_s(uint32_t x, uint32_t b0, uint32_t b1s) const {
-    const uint32_t th = (uint32_t)__mulhi((int)x, (int)b0) + x * b1s;
+    uint32_t hi;
+    if constexpr (ASM)
+      asm volatile("v_mul_hi_i32 %0, %1, %2" : "=v"(hi) : "v"(x), "v"(b0));
+    else
+      hi = (uint32_t)__mulhi((int)x, (int)b0);
+    const uint32_t th = hi + x * b1s;
     return (uint32_t)(((uint64_t)th * q + as) >> 32);
   }
   __device__ __forceinline__ uint32_t shoup(uint32_t x, uint32_t b0, uint32_t b1) const {
@@ -366,7 +375,7 @@ struct Arith32P {
   // CT (ntt.C:365-367 pattern): X in [0, 2q) (XC: canonical; XN: signed in (-q, q)), Y any ->
   // X' in [0, 2q), Y' in (0, 2q) (YN: x - t signed in (-q, q), for a register whose next use is
   // as the X of a butterfly, where the carry of x + q corrects it as cheaply as csub would)
-  template <bool XC = false, bool XN = false, bool YN = false>
+  template <bool XC = false, bool XN = false, bool YN = false, bool ASM = false>
   __device__ __forceinline__ void ct(uint32_t &X, uint32_t &Y, uint32_t b0, uint32_t b1) const {
     uint32_t x;
     if (XC) {
@@ -378,7 +387,7 @@ struct Arith32P {
       x = csub(X, q);
     }
     // NTTMUL_P_TYPED 2: an N-type X comes with an N-type Y and a signed-form twiddle pair
-    const uint32_t t = XN && NTTMUL_P_TYPED >= 2 ? pmul_s(Y, b0, b1) : pmul(Y, b0, b1);
+    const uint32_t t = XN && NTTMUL_P_TYPED >= 2 ? pmul_s<ASM>(Y, b0, b1) : pmul(Y, b0, b1);
     X = x + t;
     Y = YN ? x - t : x - t + q;
   }

@@ -97,3 +97,34 @@ def test_bank_census(logs, expected):
     Gr = Groups(logs)
     total = sum(_extra_cycles(Gr, x, g) for x in range(Gr.G - 1) for g in (x, x + 1))
     assert total == expected
+
+
+class GroupsWT(Groups):
+    """kernels.hip Groups<12, WT=true> (NTTMUL_WAVE_TYPED, an A/B variant): groups 1 and 2 take
+    the type bit of the previous group's last stage (element bit 8 / 4) from thread bit 6."""
+
+    def base(self, g, j):
+        if g == 1:
+            return ((j & 15) + (((j >> 4) & 1) << 9) + (((j >> 5) & 1) << 10) +
+                    (((j >> 6) & 1) << 8) + (((j >> 7) & 1) << 11))
+        if g == 2:
+            return ((j & 63) << 5) + (((j >> 6) & 1) << 4) + (((j >> 7) & 1) << 11)
+        return super().base(g, j)
+
+    def padx(self, x, e):
+        return e + (e >> 5)
+
+
+def test_wave_typed_layouts():
+    """The WT layouts are bijective and bit-disjoint, the type bit is wave-uniform (thread bit 6,
+    the same for all 64 lanes of a wave), and e + (e >> 5) is conflict-free on both exchanges."""
+    Gr = GroupsWT(12)
+    for g in range(3):
+        elems = sorted(Gr.base(g, j) + Gr.off(g, k) for j in range(Gr.TP) for k in range(16))
+        assert elems == list(range(Gr.N))
+        assert all(Gr.base(g, j) & Gr.off(g, k) == 0 for j in range(Gr.TP) for k in range(16))
+    for g, bit in ((1, 8), (2, 4)):
+        for w in range(4):
+            types = {(Gr.base(g, j) >> bit) & 1 for j in range(64 * w, 64 * w + 64)}
+            assert len(types) == 1 and types == {(w & 1)}
+    assert sum(_extra_cycles(Gr, x, g) for x in range(2) for g in (x, x + 1)) == 0
