@@ -1054,9 +1054,9 @@ __global__ __launch_bounds__(256) void k_cols_inv(KParams<A> P,
 // waits vmcnt(0), the workgroup barriers, and one lane adds 1 (agent scope) to the polynomial's
 // counter; a consumer's lane 0 polls that counter with sc1 loads, then the workgroup barriers.
 // Every scratch word is written once and read once per launch (no address reuse inside a
-// launch).  A poll that has not seen its count after ~2^24 polls (far beyond any wait of a
-// correct schedule) records a fault flag and gives up, so a bug ends the launch instead of
-// hanging the GPU.
+// launch).  A poll that has not seen its count after 2^20 polls (tens of ms to ~1 s, far beyond
+// any wait of a correct schedule) records a fault flag and gives up, so a bug ends the launch
+// instead of hanging the GPU.
 constexpr int kMpCols = 16;  // column tasks per polynomial: 4096 columns / 256 threads
 struct MpSync {
   unsigned *head;            // ticket counter (zeroed before the launch)
@@ -1105,7 +1105,7 @@ __device__ __forceinline__ void mp_wait(const MpSync &S, const unsigned *cnt, un
     unsigned polls = 0;
     while (__hip_atomic_load((unsigned *)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
       __builtin_amdgcn_s_sleep(2);
-      if (++polls == (1u << 24)) {
+      if (++polls == (1u << 20)) {  // >= 60 ms of polling: far beyond any correct wait
         __hip_atomic_store(S.fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }

@@ -585,10 +585,14 @@ int run_host(nttmul_ctx *ctx, int op, void *c, const void *a, const void *b, siz
   std::vector<std::thread> th;
   for (int i = 1; i < ctx->ndev; i++) {
     const size_t p0 = batch * (size_t)i / ctx->ndev, p1 = batch * (size_t)(i + 1) / ctx->ndev;
-    if (p1 > p0)
+    if (p1 <= p0) continue;
+    try {
       th.emplace_back([ctx, &J, &status, i, p0, p1] {
         status[i] = run_host_dev(ctx, ctx->dev[i], J, p0, p1);
       });
+    } catch (...) {  // no thread available: this slice runs on the caller's thread
+      status[i] = run_host_dev(ctx, ctx->dev[i], J, p0, p1);
+    }
   }
   const size_t p1 = batch / ctx->ndev;
   if (p1 > 0) status[0] = run_host_dev(ctx, ctx->dev[0], J, 0, p1);
