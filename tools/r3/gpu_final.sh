@@ -1,0 +1,12 @@
+# Round-3 evidence for the current build: GPU parity tests, smoke, then bench lines + rocprofv3
+# kernel stats + PMC passes (tools/gpu_prof.sh) for C3, C5, C2 and the two-stream C2 line.
+set -o pipefail
+TAG=${1:-r3final}
+OUT=gpurun_out/$TAG; mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || { tail -60 $OUT/gpu_tests.log; exit 1; }
+tail -2 $OUT/gpu_tests.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -20 $OUT/smoke.log; exit 1; }
+tail -1 $OUT/smoke.log
+bash tools/gpu_prof.sh $TAG c3 c5 c2 c2s 2> $OUT/prof.log || { tail -30 $OUT/prof.log; exit 1; }
+tail -5 $OUT/prof.log
