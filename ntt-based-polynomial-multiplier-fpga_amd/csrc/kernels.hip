@@ -99,11 +99,16 @@
 #ifndef NTTMUL_ABL_BOUNDQ
 #define NTTMUL_ABL_BOUNDQ 0
 #endif
+// LDS exchanges replaced by the register/lane transposes an intra-wave exchange needs (wrong
+// results: prices the one-wave-per-product form's exchanges, see perm_xchg)
+#ifndef NTTMUL_ABL_PERMXCHG
+#define NTTMUL_ABL_PERMXCHG 0
+#endif
 // The ablation switches above give wrong products by design: they compile only into the
 // tools/kbench timing binaries (tools/kbench/build.sh passes NTTMUL_KBENCH_BUILD), never into
 // libnttmul.so
 #if (NTTMUL_ABL_TWMASK || NTTMUL_ABL_NOLOAD || NTTMUL_ABL_NOXCHG || NTTMUL_ABL_NOSTORE || \
-     NTTMUL_ABL_BOUNDQ || \
+     NTTMUL_ABL_BOUNDQ || NTTMUL_ABL_PERMXCHG || \
      NTTMUL_KBENCH_LITE || defined(NTTMUL_ABL_L2LOAD) || defined(NTTMUL_STAGGER)) && \
     !defined(NTTMUL_KBENCH_BUILD)
 #error "NTTMUL_ABL_* / NTTMUL_KBENCH_LITE are wrong-result kbench switches (tools/kbench/build.sh only)"
@@ -494,11 +499,57 @@ __device__ __forceinline__ void xsync() {
   }
 }
 
+#if NTTMUL_ABL_PERMXCHG
+// Pricing ablation for exchanges inside a wavefront (the one-wave-per-product form): the four
+// register bits of a 16-register group trade places with lane bits 5, 4, 3 and 0 through
+// v_permlane32_swap, v_permlane16_swap and DPP row_ror:8 / quad_perm [1,0,3,2] -- the same
+// instruction count a real intra-wave exchange of 4 bits needs -- in place of the LDS round trip
+// (wrong results: the lanes are not the partners the layout needs)
+template <int DPP, int LB, int RB, int K = 0>
+__device__ __forceinline__ void perm_dpp(uint32_t (&r)[16], bool lb) {
+  if constexpr (K < 16) {
+    if constexpr (!(K & (1 << RB))) {
+      constexpr int K1 = K | (1 << RB);
+      const uint32_t send = lb ? r[K] : r[K1];
+      const uint32_t recv = (uint32_t)__builtin_amdgcn_mov_dpp((int)send, DPP, 0xf, 0xf, false);
+      r[K] = lb ? recv : r[K];
+      r[K1] = lb ? r[K1] : recv;
+    }
+    perm_dpp<DPP, LB, RB, K + 1>(r, lb);
+  }
+}
+__device__ __forceinline__ void perm_xchg32(uint32_t (&r)[16], int lane) {
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    auto s = __builtin_amdgcn_permlane32_swap(r[k], r[k + 8], false, false);
+    r[k] = s[0], r[k + 8] = s[1];
+  }
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    if (k & 4) continue;
+    auto s = __builtin_amdgcn_permlane16_swap(r[k], r[k + 4], false, false);
+    r[k] = s[0], r[k + 4] = s[1];
+  }
+  perm_dpp<0x128, 3, 1>(r, (lane >> 3) & 1);  // row_ror:8 = lane xor 8
+  perm_dpp<0xB1, 0, 0>(r, lane & 1);          // quad_perm [1,0,3,2] = lane xor 1
+}
+template <class W>
+__device__ __forceinline__ void perm_xchg(W (&x)[16], int lane) {
+  static_assert(sizeof(W) == 4, "priced for 32-bit words (C2, C3)");
+  perm_xchg32(x, lane);
+}
+#endif
+
 // Move 16 registers of each region from layout gfrom to layout gto through LDS.
 template <int LOGS, int gfrom, int gto, int NREG, class W, int SYNC = 0, bool WT = false>
 __device__ __forceinline__ void exchange(W (&x)[16], W (&y)[16], W *lds_x, W *lds_y, int j) {
   using Gr = Groups<LOGS, WT>;
 #if NTTMUL_ABL_NOXCHG
+  return;
+#endif
+#if NTTMUL_ABL_PERMXCHG
+  perm_xchg(x, j & 63);
+  if (NREG == 2) perm_xchg(y, j & 63);
   return;
 #endif
   constexpr int X = gfrom < gto ? gfrom : gto;
@@ -900,6 +951,57 @@ __global__ __launch_bounds__(256) void k_rows_pipe(KParams<A> P, const uint32_t 
       x[k] = nx[k];
       y[k] = ny[k];
     }
+  }
+}
+
+// Two waves per product (n = 1024, u32 words): wave 0 transforms a, wave 1 transforms b at the
+// same time, wave 1 hands its transformed b to wave 0 through LDS (register k of lane j at word
+// 64 k + j: the same element in both waves) and exits; wave 0 multiplies, runs the inverse and
+// stores.  Each wave holds one polynomial, so twice the waves fit per SIMD, and the longest
+// per-wave chain is two thirds of a product's work instead of all of it.
+template <class A, int LOGS>
+__global__ __launch_bounds__(128) void k_rows_ab(KParams<A> P, const uint32_t *__restrict__ a,
+                                                 const uint32_t *__restrict__ b,
+                                                 uint32_t *__restrict__ c, size_t units) {
+  using W = typename A::word;
+  static_assert(sizeof(W) == 4, "u32 products");
+  using Gr = Groups<LOGS, kWT<A, LOGS>()>;
+  constexpr int N = Gr::N, NP = Gr::NP, G = Gr::G;
+  static_assert(N / 16 == 64 && NP >= N, "one wave per polynomial");
+  __shared__ W xch[2][NP];
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), j = threadIdx.x & 63;
+  const size_t u = blockIdx.x;
+  if (u >= units) return;  // block-uniform
+  W *lx = xch[wv];
+  constexpr int kAux = NTTMUL_CPOL < 0 ? 0 : NTTMUL_CPOL;
+  constexpr int kAuxSt = NTTMUL_CPOL_ST < 0 ? 0 : NTTMUL_CPOL_ST;
+  W x[16], y[16];
+  {
+    const auto r = span_rsrc((wv ? b : a) + u * N, N);
+#pragma unroll
+    for (int k = 0; k < 16; k++) x[k] = (W)buf_ld32<kAux>(r, (Gr::base(0, j) + Gr::off(0, k)) * 4);
+  }
+  constexpr int D = NTTMUL_BASE_D ? A::kBaseD : 0;
+  TwPair<W> zw[16];
+  fwd_all<A, LOGS, 0, 1, D, 1>(P.ar, x, y, lx, lx, P.fw, j, 0, 0, zw);
+  if (wv) {
+    W *t = xch[1];
+    xsync<1>();  // wave 1's last exchange reads are done before the region is overwritten
+#pragma unroll
+    for (int k = 0; k < 16; k++) t[k * 64 + j] = x[k];
+  }
+  __syncthreads();
+  if (wv) return;
+#pragma unroll
+  for (int k = 0; k < 16; k++) y[k] = xch[1][k * 64 + j];
+  base_mult<A, LOGS, D>(P.ar, x, y, zw, j);
+  inv_all<A, LOGS, G - 1, true, D, 1>(P, x, y, lx, lx, P.iw, j, 0, 0);
+  const auto rc = span_rsrc(c + u * N, N);
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    W v = x[k];
+    if (!A::kInvCanonical) v = P.ar.canon(v);
+    buf_st32<kAuxSt>(rc, (Gr::base(0, j) + Gr::off(0, k)) * 4, (uint32_t)v);
   }
 }
 
@@ -1375,6 +1477,16 @@ static hipError_t fused(const LaunchTables &T, const void *a, const void *b, voi
   if constexpr (std::is_same<A, Arith32P>::value && std::is_same<IO, uint32_t>::value) {
     if (T.logn == 10 && T.pipe_per_wave > 0)
       return launch_pipe<A>(P, a, b, c, batch, T.pipe_per_wave, s);
+    if (T.logn == 10 && T.pipe_per_wave == -2) {  // k_rows_ab
+      if (tl_describe) {
+        describe_add(std::string("k_rows_ab<") + AName<A>::v + ",10>");
+        return hipSuccess;
+      }
+      if (batch == 0) return hipSuccess;
+      hipLaunchKernelGGL((k_rows_ab<A, 10>), dim3((unsigned)batch), dim3(128), 0, s, P,
+                         (const uint32_t *)a, (const uint32_t *)b, (uint32_t *)c, batch);
+      return hipGetLastError();
+    }
     if (T.logn == 10 && T.pipe_per_wave < 0) {  // k_rows_w4
       if (tl_describe) {
         describe_add(std::string("k_rows_w4<") + AName<A>::v + ",10>");

@@ -133,29 +133,67 @@ def load_library() -> ctypes.CDLL:
     return lib
 
 
-def code_object_id(path: str = LIB_PATH) -> str:
-    """Identity of the device code in libnttmul.so: sha256 (16 hex digits) of its .hip_fatbin
-    section, the gfx950 code objects of every kernel.  Host-only changes keep it; any kernel
-    change alters it.  bench.py keys the committed PMC/ISA profiles (profiles/) by it, so a
-    profile of another build is never reported as this build's."""
-    import hashlib
+def _elf_sections(elf: bytes) -> dict:
+    """{section name: bytes} of an ELF64 image (NOBITS sections map to b"")."""
     import struct
-    with open(path, "rb") as f:
-        elf = f.read()
     if elf[:4] != b"\x7fELF" or elf[4] != 2:
-        raise ValueError(f"{path}: not an ELF64 file")
+        raise ValueError("not an ELF64 image")
     shoff, = struct.unpack_from("<Q", elf, 0x28)
     shentsize, shnum, shstrndx = struct.unpack_from("<HHH", elf, 0x3A)
 
     def sec(i):
-        name, _, _, _, off, size = struct.unpack_from("<IIQQQQ", elf, shoff + i * shentsize)
-        return name, off, size
-    _, stroff, _ = sec(shstrndx)
+        return struct.unpack_from("<IIQQQQ", elf, shoff + i * shentsize)
+    stroff = sec(shstrndx)[4]
+    out = {}
     for i in range(shnum):
-        name, off, size = sec(i)
-        if elf[stroff + name:elf.index(b"\0", stroff + name)] == b".hip_fatbin":
-            return hashlib.sha256(elf[off:off + size]).hexdigest()[:16]
-    raise ValueError(f"{path}: no .hip_fatbin section")
+        name, typ, _, _, off, size = sec(i)
+        key = elf[stroff + name:elf.index(b"\0", stroff + name)].decode(errors="replace")
+        out[key] = b"" if typ == 8 else elf[off:off + size]
+    return out
+
+
+_BUNDLE_MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+
+def _device_code(fatbin: bytes):
+    """The machine-code sections (.text, .rodata kernel descriptors, .note kernel metadata) of
+    every amdgcn code object in a .hip_fatbin section, concatenated in bundle order; or None
+    when the section holds no parsable offload bundle."""
+    import struct
+    parts, pos = [], fatbin.find(_BUNDLE_MAGIC)
+    while pos >= 0:
+        n, = struct.unpack_from("<Q", fatbin, pos + 24)
+        cur = pos + 32
+        for _ in range(n):
+            off, size, tlen = struct.unpack_from("<QQQ", fatbin, cur)
+            triple = fatbin[cur + 24:cur + 24 + tlen]
+            cur += 24 + tlen
+            if b"amdgcn" in triple and size:
+                secs = _elf_sections(fatbin[pos + off:pos + off + size])
+                parts += [triple] + [secs.get(k, b"") for k in (".text", ".rodata", ".note")]
+        pos = fatbin.find(_BUNDLE_MAGIC, cur)
+    return b"".join(parts) if parts else None
+
+
+def code_object_id(path: str = LIB_PATH) -> str:
+    """Identity of the device code in libnttmul.so: sha256 (16 hex digits) of the machine code of
+    its gfx950 code objects -- each one's .text, .rodata (kernel descriptors) and .note (kernel
+    metadata: names, register and LDS counts) -- read from the .hip_fatbin section's offload
+    bundles (the whole section when it holds none).  Symbol tables are left out: they carry
+    the compiler's per-source `__hip_cuid_*` marker, which changes with any edit of the .hip
+    file even when no kernel does.  Host-only changes keep the id; any kernel change alters it.
+    bench.py keys the committed PMC/ISA profiles (profiles/) by it, so a profile of another
+    build is never reported as this build's."""
+    import hashlib
+    with open(path, "rb") as f:
+        elf = f.read()
+    if elf[:4] != b"\x7fELF" or elf[4] != 2:
+        raise ValueError(f"{path}: not an ELF64 file")
+    fat = _elf_sections(elf).get(".hip_fatbin")
+    if fat is None:
+        raise ValueError(f"{path}: no .hip_fatbin section")
+    code = _device_code(fat)
+    return hashlib.sha256(fat if code is None else code).hexdigest()[:16]
 
 
 def exported_symbols() -> list:

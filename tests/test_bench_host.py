@@ -27,26 +27,60 @@ def test_workload_names():
     assert bench.workload_name(2048, 2013265921, 10, 1) == "custom"
 
 
-def _elf_with_fatbin(path, payload: bytes):
-    """A minimal ELF64 with a .shstrtab and a .hip_fatbin section."""
-    names = b"\0.shstrtab\0.hip_fatbin\0"
-    data_off = 64
-    fat_off = data_off + len(names)
-    sh_off = fat_off + len(payload)
-    sh_off += (-sh_off) % 8
+def _elf(sections: dict) -> bytes:
+    """A minimal ELF64 image holding a .shstrtab and the given {name: bytes} sections."""
+    names = b"\0.shstrtab\0" + b"".join(k.encode() + b"\0" for k in sections)
+    blobs, off = [], 64 + len(names)
+    for data in sections.values():
+        blobs.append((off, data))
+        off += len(data)
+    sh_off = off + (-off) % 8
+    nsec = 2 + len(sections)
     hdr = bytearray(64)
     hdr[:4] = b"\x7fELF"
     hdr[4] = 2                                   # ELFCLASS64
     hdr[5] = 1
     struct.pack_into("<Q", hdr, 0x28, sh_off)    # e_shoff
-    struct.pack_into("<HHH", hdr, 0x3A, 64, 3, 1)  # e_shentsize, e_shnum, e_shstrndx
-    secs = bytearray(64 * 3)
-    struct.pack_into("<IIQQQQ", secs, 64, 1, 3, 0, 0, data_off, len(names))     # .shstrtab
-    struct.pack_into("<IIQQQQ", secs, 128, 11, 1, 0, 0, fat_off, len(payload))  # .hip_fatbin
-    body = bytes(hdr) + names + payload
-    body += b"\0" * (sh_off - len(body))
+    struct.pack_into("<HHH", hdr, 0x3A, 64, nsec, 1)  # e_shentsize, e_shnum, e_shstrndx
+    secs = bytearray(64 * nsec)
+    struct.pack_into("<IIQQQQ", secs, 64, 1, 3, 0, 0, 64, len(names))         # .shstrtab
+    name_off = 11
+    for i, (k, (o, data)) in enumerate(zip(sections, blobs)):
+        struct.pack_into("<IIQQQQ", secs, 64 * (2 + i), name_off, 1, 0, 0, o, len(data))
+        name_off += len(k) + 1
+    body = bytes(hdr) + names + b"".join(d for _, d in blobs)
+    return body + b"\0" * (sh_off - len(body)) + bytes(secs)
+
+
+def _elf_with_fatbin(path, payload: bytes):
+    """A minimal ELF64 with a .hip_fatbin section."""
     with open(path, "wb") as f:
-        f.write(body + bytes(secs))
+        f.write(_elf({".hip_fatbin": payload}))
+
+
+def _bundle(entries) -> bytes:
+    """A clang offload bundle of (triple, image) entries."""
+    head = len(b"__CLANG_OFFLOAD_BUNDLE__") + 8 + sum(24 + len(t) for t, _ in entries)
+    out, table, off = b"", b"", head
+    for triple, image in entries:
+        table += struct.pack("<QQQ", off, len(image), len(triple)) + triple
+        off += len(image)
+    out = b"__CLANG_OFFLOAD_BUNDLE__" + struct.pack("<Q", len(entries)) + table
+    return out + b"".join(image for _, image in entries)
+
+
+def test_code_object_id_reads_machine_code(tmp_path):
+    """The id follows each amdgcn code object's .text / .rodata / .note and ignores its symbol
+    tables (the compiler's __hip_cuid_* marker changes with any source edit) and host entries."""
+    def lib(path, text, dynsym, host=b"host"):
+        co = _elf({".note": b"meta", ".dynsym": dynsym, ".rodata": b"kd", ".text": text})
+        _elf_with_fatbin(path, _bundle([(b"host-x86_64-unknown-linux-gnu-", host),
+                                        (b"hipv4-amdgcn-amd-amdhsa--gfx950", co)]))
+        return nttmul.code_object_id(str(path))
+    base = lib(tmp_path / "a.so", b"\x01\x02", b"__hip_cuid_1111")
+    assert lib(tmp_path / "b.so", b"\x01\x02", b"__hip_cuid_2222") == base   # cuid only
+    assert lib(tmp_path / "c.so", b"\x01\x02", b"__hip_cuid_1111", b"h2") == base
+    assert lib(tmp_path / "d.so", b"\x01\x03", b"__hip_cuid_1111") != base   # a kernel changed
 
 
 def test_code_object_id(tmp_path):
