@@ -22,16 +22,16 @@ one() {  # cfg name, bench args...
   run 300 python bench.py "$@" > $OUT/bench.json 2> $OUT/bench.err
   tail -c 700 $OUT/bench.json >&2
   run 300 rocprofv3 --kernel-trace --stats -T -d $OUT/trace -o trace --output-format csv -- \
-    python3 bench.py --no-cpu-baseline --power-seconds 0 "$@" --steps 100 --warmup 20 > $OUT/trace.log 2>&1
+    python3 bench.py --no-cpu-baseline --power-seconds 0 "$@" > $OUT/trace.log 2>&1
   run 900 tools/profile_pmc.sh $OUT/pmc "$@" --no-cpu-baseline --power-seconds 0 --steps 3 --warmup 1 > $OUT/pmc.log 2>&1
 }
 for cfg in $CFGS; do
   case $cfg in
     c3) one c3 ;;
-    c5) one c5 --n 65536 --q 4611686018425815041 --batch-per-gpu 1024 --steps 30 --warmup 10 ;;
-    c2) one c2 --n 1024 --batch-per-gpu 4096 --steps 300 --warmup 50 ;;
+    c5) one c5 --n 65536 --q 4611686018425815041 --batch-per-gpu 1024 --steps 200 --warmup 100 ;;
+    c2) one c2 --n 1024 --batch-per-gpu 4096 --steps 3000 --warmup 2000 ;;
     c2s) mkdir -p gpurun_out/$TAG/c2s  # two streams: bench line only (same kernel as c2)
-         run 300 python bench.py --n 1024 --batch-per-gpu 4096 --steps 300 --warmup 50 --streams 2 \
+         run 300 python bench.py --n 1024 --batch-per-gpu 4096 --steps 3000 --warmup 2000 --streams 2 \
            --no-cpu-baseline > gpurun_out/$TAG/c2s/bench.json 2> gpurun_out/$TAG/c2s/bench.err
          tail -c 400 gpurun_out/$TAG/c2s/bench.json >&2 ;;
   esac
