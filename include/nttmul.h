@@ -86,8 +86,12 @@ int nttmul_get_info(const nttmul_ctx *ctx, nttmul_info *info);
 /* Diagnostics (no reference counterpart): the device kernel(s) one product call with word_bits
  * storage dispatches to, as rocprofv3 names them with template arguments, e.g.
  * "k_rows<Arith32P3,u32,u32,12,0>" (n > 4096: the passes joined by " + ").  Copies at most
- * cap - 1 characters and a NUL into buf; returns the full length, or a negative status. */
+ * cap - 1 characters and a NUL into buf; returns the full length, or a negative status.
+ * nttmul_kernel_name describes a large batch; nttmul_kernel_name_batch the given one (batches of
+ * at most 4 waves per SIMD run the issue-prioritised variant, named "...,prio>"). */
 int nttmul_kernel_name(const nttmul_ctx *ctx, int word_bits, char *buf, size_t cap);
+int nttmul_kernel_name_batch(const nttmul_ctx *ctx, int word_bits, size_t batch, char *buf,
+                             size_t cap);
 /* Diagnostics: how the last host-buffer call on ctx moved its first chunk: 0 staged through
  * pinned buffers, 1 direct DMA from / to page-locked caller memory, 2 zero-copy kernel access to
  * the pinned staging buffers; -1 before any call. */

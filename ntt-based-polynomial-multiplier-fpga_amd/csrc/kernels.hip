@@ -21,6 +21,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+#include <cstdlib>
 #include <string>
 #include <type_traits>
 
@@ -694,16 +696,28 @@ __host__ __device__ constexpr int rows_threads(int logs) {
 #error "NTTMUL_WAVE_TRACE is a tools/kbench instrumentation switch"
 #endif
 __device__ unsigned long long g_wave_trace[16384 * 4];
+__device__ unsigned g_wave_slot[16384];  // HW_ID (wave slot, SIMD, CU, SH, SE) | XCC_ID << 24
 hipError_t read_wave_trace(void *dst, size_t bytes) {
   return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_wave_trace), bytes);
 }
+hipError_t read_wave_slots(void *dst, size_t bytes) {
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_wave_slot), bytes);
+}
+__device__ __forceinline__ unsigned wave_slot() {
+  unsigned hw, xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  return (hw & 0xFFFFFFu) | ((xcc & 0xFu) << 24);
+}
 #define WTRACE(k) \
-  do { if (LOGS == 10 && j == 0 && u < 16384) g_wave_trace[u * 4 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+  do { if (LOGS == 10 && j == 0 && u < 16384) { \
+    g_wave_trace[u * 4 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    if ((k) == 0) g_wave_slot[u] = wave_slot(); } } while (0)
 #else
 #define WTRACE(k) do { } while (0)
 #endif
 
-template <class A, class TIn, class TOut, int LOGS, int L1>
+template <class A, class TIn, class TOut, int LOGS, int L1, bool PRIO = false>
 __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
     KParams<A> P, const TIn *__restrict__ a, const TIn *__restrict__ b, TOut *__restrict__ c,
     size_t units) {
@@ -728,6 +742,7 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
 #endif
 
   WTRACE(0);
+  if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);  // rows_prio
 #ifdef NTTMUL_STAGGER  // kbench experiment: one-wave blocks of generation blockIdx / 1024 wait
   if constexpr (LOGS == 10 && L1 == 0)
     for (unsigned i = 0; i < (blockIdx.x >> 10) * NTTMUL_STAGGER; i++) __builtin_amdgcn_s_sleep(8);
@@ -789,7 +804,9 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
   } else {
     fwd_all<A, LOGS, 0, 2, D>(P.ar, x, y, lx, ly, P.fw, j, row, L1, zw);
   }
+  if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
   base_mult<A, LOGS, D>(P.ar, x, y, zw, j);
+  if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
   inv_all<A, LOGS, G - 1, L1 == 0, D>(P, x, y, lx, ly, P.iw, j, row, L1);
   WTRACE(2);
 #if NTTMUL_ABL_NOSTORE
@@ -1433,17 +1450,59 @@ static KParams<A> product_params(const LaunchTables &T) {
   return P;
 }
 
+// Issue priority of the fused product (k_rows, L1 = 0).  The wave scheduler issues the oldest
+// ready wave first, so of the waves a SIMD holds the first finishes long before the last, which
+// then runs its tail alone with no other wave to hide its latencies: at C2 (n = 1024 x 4096, one
+// generation of 4 waves per SIMD) the four waves of a SIMD computed in 7.1 / 9.3 / 11.8 / 14.5 us
+// (tools/kbench per-SIMD trace, profiles/r3/c2/wave_trace_slots.txt).  With P.prio each wave
+// drops its priority as it completes phases (3 for the forward transforms, 1 for the base
+// multiplication, 0 for the inverse; k_rows<..., PRIO = true>), so the waves that are behind
+// issue first and all finish together: C2 17.6 vs 18.6 us; n = 512 x 8192, 256 x 16384, 2048 x 2048, 4096 x 1024 +4..9 %
+// (profiles/r3/c2/prio_ab2.txt).  It only pays when the launch is one thin generation: at 8
+// waves per SIMD (n = 1024 x 8192, 4096 x 2048) or many generations (C3, 1024 x 262144) the
+// oldest-first order is 1-7 % faster (a finished wave frees its slot early, and the loads of the
+// next block overlap the others' arithmetic).  So: on when the launch has at most 4 waves per
+// SIMD of the device (NTTMUL_PRIO=0 / 1 forces it off / on, for A/B runs).
+static bool rows_prio(size_t waves) {
+  static const int forced = [] {
+    const char *e = getenv("NTTMUL_PRIO");
+    return e && *e ? atoi(e) : -1;
+  }();
+  if (forced >= 0) return forced > 0;
+  static std::atomic<int> cus[64];  // per device; 0 = not yet queried
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+  int n = cus[dev].load(std::memory_order_relaxed);
+  if (n == 0) {
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      return false;
+    cus[dev].store(n, std::memory_order_relaxed);
+  }
+  return waves <= (size_t)n * 4 * 4;  // 4 SIMDs per CU, 4 waves per SIMD
+}
+
 template <class A, class TIn, class TOut, int LOGS, int L1>
 static hipError_t launch_rows(const KParams<A> &P, const void *a, const void *b, void *c,
                               size_t units, hipStream_t s) {
   constexpr int NT = rows_threads(LOGS), PB = NT / ((1 << LOGS) / 16);
   const size_t blocks = (units + PB - 1) / PB;
+  // (the prioritised variant exists for the u32 Plantard products only: q < 2^31, C2 / C3 family)
+  constexpr bool kPrioOk = L1 == 0 && IsPlantard<A>::value && sizeof(TIn) == 4 && sizeof(TOut) == 4;
+  const bool prio = kPrioOk && blocks && rows_prio(blocks * (NT / 64));
   if (tl_describe) {
     describe_add(std::string("k_rows<") + AName<A>::v + "," + word_name<TIn>() + "," +
-                 word_name<TOut>() + "," + std::to_string(LOGS) + "," + std::to_string(L1) + ">");
+                 word_name<TOut>() + "," + std::to_string(LOGS) + "," + std::to_string(L1) +
+                 (prio ? ",prio>" : ">"));
     return hipSuccess;
   }
   if (blocks == 0) return hipSuccess;
+  if constexpr (kPrioOk) {
+    if (prio) {
+      hipLaunchKernelGGL((k_rows<A, TIn, TOut, LOGS, L1, true>), dim3((unsigned)blocks), dim3(NT), 0,
+                         s, P, (const TIn *)a, (const TIn *)b, (TOut *)c, units);
+      return hipGetLastError();
+    }
+  }
   hipLaunchKernelGGL((k_rows<A, TIn, TOut, LOGS, L1>), dim3((unsigned)blocks), dim3(NT), 0, s, P,
                      (const TIn *)a, (const TIn *)b, (TOut *)c, units);
   return hipGetLastError();
@@ -1644,11 +1703,12 @@ hipError_t launch_polymul(const LaunchTables &T, const void *a, const void *b, v
 #endif
 }
 
-hipError_t describe_polymul(const LaunchTables &T, int io_bits, std::string *out) {
+hipError_t describe_polymul(const LaunchTables &T, int io_bits, size_t batch, std::string *out) {
   out->clear();
   void *scr[4] = {nullptr, nullptr, nullptr, (void *)out};  // (non-null: the persistent form)
   tl_describe = out;
-  const hipError_t e = launch_polymul(T, nullptr, nullptr, nullptr, 1, io_bits, scr, nullptr);
+  const hipError_t e = launch_polymul(T, nullptr, nullptr, nullptr, batch ? batch : (size_t)1 << 24,
+                                      io_bits, scr, nullptr);
   tl_describe = nullptr;
   return e;
 }

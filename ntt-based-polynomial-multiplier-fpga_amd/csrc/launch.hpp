@@ -40,7 +40,7 @@ hipError_t launch_polymul(const LaunchTables &T, const void *a, const void *b, v
                           size_t batch, int io_bits, void **scr, hipStream_t s);
 // The kernels launch_polymul would launch for (T, io_bits), as "k_rows<Arith32P3,u32,u32,12,0>"
 // (multi-pass: the three kernels joined by " + "); nothing is launched.
-hipError_t describe_polymul(const LaunchTables &T, int io_bits, std::string *out);
+hipError_t describe_polymul(const LaunchTables &T, int io_bits, size_t batch, std::string *out);
 // Standalone forward (inverse = 0) or inverse (inverse = 1) NTT of `batch` polynomials
 // (SURVEY §8f row 1).  scr as for launch_polymul (only scr[0] is used).
 hipError_t launch_xform(const LaunchTables &T, const void *in, void *out, size_t batch,

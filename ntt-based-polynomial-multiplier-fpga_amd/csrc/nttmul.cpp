@@ -750,11 +750,14 @@ int nttmul_get_info(const nttmul_ctx *ctx, nttmul_info *info) {
 
 int nttmul_last_host_path(const nttmul_ctx *ctx) { return ctx ? ctx->last_path : NTTMUL_EINVAL; }
 
-int nttmul_kernel_name(const nttmul_ctx *ctx, int word_bits, char *buf, size_t cap) {
+int nttmul_kernel_name_batch(const nttmul_ctx *ctx, int word_bits, size_t batch, char *buf,
+                             size_t cap) {
   if (!ctx || (word_bits != 32 && word_bits != 64) || (cap && !buf)) return NTTMUL_EINVAL;
   if (word_bits == 32 && ctx->plan.q > 0xFFFFFFFFull) return NTTMUL_EINVAL;
   std::string name;
-  if (describe_polymul(tables_for(ctx, ctx->dev[0]), word_bits, &name) != hipSuccess)
+  DeviceGuard guard;  // the launch choice reads the device's CU count
+  if (hipSetDevice(ctx->dev[0].id) != hipSuccess ||
+      describe_polymul(tables_for(ctx, ctx->dev[0]), word_bits, batch, &name) != hipSuccess)
     return NTTMUL_EUNSUPPORTED;
   if (cap) {
     const size_t k = std::min(cap - 1, name.size());
@@ -762,6 +765,9 @@ int nttmul_kernel_name(const nttmul_ctx *ctx, int word_bits, char *buf, size_t c
     buf[k] = 0;
   }
   return (int)name.size();
+}
+int nttmul_kernel_name(const nttmul_ctx *ctx, int word_bits, char *buf, size_t cap) {
+  return nttmul_kernel_name_batch(ctx, word_bits, 0, buf, cap);
 }
 
 int nttmul_multiply_batch_u32(nttmul_ctx *ctx, uint32_t *c, const uint32_t *a, const uint32_t *b,

@@ -91,6 +91,7 @@ def load_library() -> ctypes.CDLL:
     lib.nttmul_last_error.restype = ctypes.c_char_p
     lib.nttmul_get_info.argtypes = [vp, ctypes.POINTER(Info)]
     lib.nttmul_kernel_name.argtypes = [vp, i32, ctypes.c_char_p, sz]
+    lib.nttmul_kernel_name_batch.argtypes = [vp, i32, sz, ctypes.c_char_p, sz]
     lib.nttmul_last_host_path.argtypes = [vp]
     for name in ("nttmul_multiply_u32", "nttmul_multiply_u64"):
         getattr(lib, name).argtypes = [vp, vp, vp, vp]
@@ -287,12 +288,13 @@ class Context:
         """nttmul_last_host_path: 0 staged, 1 direct DMA, 2 zero-copy, -1 no call yet."""
         return int(self._lib.nttmul_last_host_path(self._h))
 
-    def kernel_name(self, word_bits: int = 0) -> str:
-        """The device kernel(s) a product call dispatches to (nttmul_kernel_name), e.g.
-        "k_rows<Arith32P3,u32,u32,12,0>"."""
+    def kernel_name(self, word_bits: int = 0, batch: int = 0) -> str:
+        """The device kernel(s) a product call of `batch` polynomials dispatches to
+        (nttmul_kernel_name_batch; batch 0 = a large batch), e.g. "k_rows<Arith32P3,u32,u32,12,0>",
+        or "k_rows<Arith32P,u32,u32,10,0,prio>" for a batch of at most 4 waves per SIMD."""
         word_bits = word_bits or (32 if self.q < (1 << 32) else 64)
         buf = ctypes.create_string_buffer(256)
-        st = self._lib.nttmul_kernel_name(self._h, word_bits, buf, len(buf))
+        st = self._lib.nttmul_kernel_name_batch(self._h, word_bits, batch, buf, len(buf))
         if st < 0:
             self._check(st)
         return buf.value.decode()

@@ -282,6 +282,33 @@ def test_full_size_device_path(n, q, word_bits, batch, chunk_mb, lanes, lag, tor
     assert _check_whole_batch(n, q, word_bits, 0, batch, a, b, c) == batch
 
 
+@pytest.mark.parametrize("n,q", [(256, Q31), (512, Q31), (1024, Q31), (1024, Q30), (2048, Q31),
+                                 (4096, Q31), (4096, Q31HI)])
+def test_issue_priority_variants(n, q, torch_cuda):
+    """The fused product has two launch forms (kernels.hip rows_prio): batches of at most 4 waves
+    per SIMD run k_rows<..., PRIO = true> (issue priority lowered as each wave completes its
+    transforms), larger ones the oldest-first kernel.  On both sides of the threshold the library
+    names the kernel it launches and every product equals the oracle's."""
+    torch = torch_cuda
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    waves_per_product = max(1, n // 16 // 64)           # n / 16 threads per product
+    products_per_wave = max(1, 64 // (n // 16))
+    limit = 16 * cus * products_per_wave // waves_per_product  # 4 waves x 4 SIMDs per CU
+    ctx = _ctx(n, q)
+    stream = torch.cuda.current_stream().cuda_stream
+    for batch, prio in ((limit, True), (limit + 1 + 16, False), (7, True)):
+        name = ctx.kernel_name(32, batch)
+        assert name.endswith(",prio>") == prio, (batch, name)
+        a = torch.empty(batch * n, dtype=torch.int32, device="cuda")
+        b = torch.empty_like(a)
+        c = torch.empty_like(a)
+        ctx.fill_random_device(a, b, 0, batch, 32, stream=stream)
+        ctx.multiply_device(c, a, b, batch, 32, stream=stream)
+        torch.cuda.synchronize()
+        assert _check_whole_batch(n, q, 32, 0, batch, a, b, c) == batch
+    assert not ctx.kernel_name(32).endswith(",prio>")   # batch 0: a large batch
+
+
 @pytest.mark.parametrize("lag", MP_LAGS)
 def test_c5_bigint_golden(golden_dir, lag, torch_cuda, monkeypatch):
     """C5 products (n = 65536, q = 0x3FFFFFFFFFE80001) on the device, through the product path the

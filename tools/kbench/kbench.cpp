@@ -10,7 +10,11 @@
 #ifdef NTTMUL_WAVE_TRACE
 #include <algorithm>
 #include <vector>
-namespace nttmul { hipError_t read_wave_trace(void *dst, size_t bytes); }
+#include <map>
+namespace nttmul {
+hipError_t read_wave_trace(void *dst, size_t bytes);
+hipError_t read_wave_slots(void *dst, size_t bytes);
+}
 #endif
 
 #define CK(x)                                                                   \
@@ -132,6 +136,47 @@ int main(int argc, char **argv) {
       std::sort(v.begin(), v.end());
       printf("  %-9s p0 %6.2f  p10 %6.2f  p50 %6.2f  p90 %6.2f  p100 %6.2f us\n", nm[k], v[0],
              v[nw / 10], v[nw / 2], v[nw * 9 / 10], v[nw - 1]);
+    }
+    // waves per SIMD (HW_ID bits 4-5 SIMD, 8-11 CU, 12 SH, 13-15 SE; XCC_ID << 24), and per
+    // SIMD load: when its last wave stored, against how many waves it ran
+    std::vector<unsigned> slot(nw);
+    CK(nttmul::read_wave_slots(slot.data(), slot.size() * 4));
+    std::map<unsigned, std::vector<size_t>> simd;
+    for (size_t i = 0; i < nw; i++) simd[slot[i] & 0xF00FF30u].push_back(i);
+    std::map<size_t, std::vector<double>> by_count;  // waves on the SIMD -> its last store (us)
+    std::map<unsigned, int> per_cu;
+    for (auto &kv : simd) {
+      double last = 0;
+      for (size_t i : kv.second) last = std::max(last, (tr[i * 4 + 3] - t0) * 0.01);
+      by_count[kv.second.size()].push_back(last);
+      per_cu[kv.first & 0xF00FF00u] += (int)kv.second.size();
+    }
+    printf("  SIMDs used %zu, CUs used %zu\n", simd.size(), per_cu.size());
+    for (auto &kv : by_count) {
+      std::sort(kv.second.begin(), kv.second.end());
+      printf("  %zu waves on %zu SIMDs: last store p0 %6.2f p50 %6.2f p100 %6.2f us\n", kv.first,
+             kv.second.size(), kv.second[0], kv.second[kv.second.size() / 2], kv.second.back());
+    }
+    std::map<int, int> cu_hist;
+    for (auto &kv : per_cu) cu_hist[kv.second]++;
+    printf("  waves per CU:");
+    for (auto &kv : cu_hist) printf(" %d x%d", kv.first, kv.second);
+    printf("\n");
+    // within the SIMDs holding 4 waves: completion order by entry order (oldest-first issue?)
+    std::vector<double> rank_done[8];
+    for (auto &kv : simd) {
+      if (kv.second.size() != 4) continue;
+      std::vector<size_t> w = kv.second;
+      std::sort(w.begin(), w.end(), [&](size_t x, size_t y) { return tr[x * 4] < tr[y * 4]; });
+      for (size_t r = 0; r < w.size(); r++)
+        rank_done[r].push_back((tr[w[r] * 4 + 2] - tr[w[r] * 4 + 1]) * 0.01);
+    }
+    for (int r = 0; r < 4; r++) {
+      auto &v = rank_done[r];
+      if (v.empty()) continue;
+      std::sort(v.begin(), v.end());
+      printf("  4-wave SIMDs, wave %d by entry: compute (loaded->computed) p50 %6.2f us\n", r,
+             v[v.size() / 2]);
     }
   }
 #endif
