@@ -21,7 +21,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <atomic>
 #include <cstdlib>
 #include <string>
 #include <type_traits>
@@ -1462,23 +1461,17 @@ static KParams<A> product_params(const LaunchTables &T) {
 // waves per SIMD (n = 1024 x 8192, 4096 x 2048) or many generations (C3, 1024 x 262144) the
 // oldest-first order is 1-7 % faster (a finished wave frees its slot early, and the loads of the
 // next block overlap the others' arithmetic).  So: on when the launch has at most 4 waves per
-// SIMD of the device (NTTMUL_PRIO=0 / 1 forces it off / on, for A/B runs).
+// SIMD of the device and no other product launch of the context may still be running on
+// another stream (T.prio_ok, nttmul.cpp run_device: two streams of C2 launches overlap, and then
+// the oldest-first order wins, 292 vs 262 M/s); NTTMUL_PRIO=0 / 1 forces it off / on.
+static thread_local int tl_prio_cus = 0;  // launch_polymul: T.cus, or 0 when T.prio_ok is 0
 static bool rows_prio(size_t waves) {
   static const int forced = [] {
     const char *e = getenv("NTTMUL_PRIO");
     return e && *e ? atoi(e) : -1;
   }();
   if (forced >= 0) return forced > 0;
-  static std::atomic<int> cus[64];  // per device; 0 = not yet queried
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
-  int n = cus[dev].load(std::memory_order_relaxed);
-  if (n == 0) {
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      return false;
-    cus[dev].store(n, std::memory_order_relaxed);
-  }
-  return waves <= (size_t)n * 4 * 4;  // 4 SIMDs per CU, 4 waves per SIMD
+  return waves <= (size_t)tl_prio_cus * 4 * 4;  // 4 SIMDs per CU, 4 waves per SIMD
 }
 
 template <class A, class TIn, class TOut, int LOGS, int L1>
@@ -1674,8 +1667,18 @@ static hipError_t polymul_io(const LaunchTables &T, const void *a, const void *b
              : fused<A, uint32_t>(T, a, b, c, batch, s);
 }
 
+static hipError_t launch_polymul_(const LaunchTables &T, const void *a, const void *b, void *c,
+                                  size_t batch, int io_bits, void **scr, hipStream_t s);
 hipError_t launch_polymul(const LaunchTables &T, const void *a, const void *b, void *c,
                           size_t batch, int io_bits, void **scr, hipStream_t s) {
+  const int prev = tl_prio_cus;
+  tl_prio_cus = T.prio_ok ? T.cus : 0;
+  const hipError_t e = launch_polymul_(T, a, b, c, batch, io_bits, scr, s);
+  tl_prio_cus = prev;
+  return e;
+}
+static hipError_t launch_polymul_(const LaunchTables &T, const void *a, const void *b, void *c,
+                                  size_t batch, int io_bits, void **scr, hipStream_t s) {
 #if NTTMUL_KBENCH_LITE == 2  // tools/kbench C5 builds: 64-bit words, n = 65536 only
   if (T.word_bits != 64 || T.logn != 16 || io_bits != 64) return hipErrorNotSupported;
   return multipass<Arith64, uint64_t>(T, a, b, c, batch, scr, s);

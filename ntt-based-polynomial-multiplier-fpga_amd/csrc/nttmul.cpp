@@ -80,6 +80,12 @@ struct DevState {
   size_t slot_bytes = 0;
   int *flag = nullptr;                        // range-check result
   int cus = 0;                                // compute units (persistent grid sizing)
+  // the last fused product launch (run_device): its stream and an event after it.  A product
+  // launched on another stream while that one may still run keeps oldest-first issue
+  // (LaunchTables::prio_ok): overlapping launches are better served by it
+  std::mutex prod_mu;
+  hipEvent_t prod_ev = nullptr;
+  hipStream_t prod_s = nullptr;
 };
 
 }  // namespace
@@ -301,7 +307,15 @@ int run_device(nttmul_ctx *ctx, DevState &d, Scratch &sc, int op, void *c, const
   }
   const bool multipass = P.logn > 12 && op != OP_POINTWISE;
   if (!multipass && !reorder) {  // one launch over the whole batch, no scratch
-    if (op == OP_MULTIPLY) HIP_TRY(ctx, launch_polymul(T, a, b, c, batch, io_bits, sc.buf, s));
+    if (op == OP_MULTIPLY) {
+      std::lock_guard<std::mutex> lk(d.prod_mu);
+      if (!d.prod_ev) HIP_TRY(ctx, hipEventCreateWithFlags(&d.prod_ev, hipEventDisableTiming));
+      if (d.prod_s && d.prod_s != s && hipEventQuery(d.prod_ev) == hipErrorNotReady) T.prio_ok = 0;
+      HIP_TRY(ctx, launch_polymul(T, a, b, c, batch, io_bits, sc.buf, s));
+      HIP_TRY(ctx, hipEventRecord(d.prod_ev, s));
+      d.prod_s = s;
+      return NTTMUL_OK;
+    }
     else if (op == OP_POINTWISE) HIP_TRY(ctx, launch_pointwise(T, a, b, c, batch, io_bits, s));
     else HIP_TRY(ctx, launch_xform(T, a, c, batch, io_bits, inv, sc.buf, s));
     return NTTMUL_OK;
@@ -723,6 +737,7 @@ void nttmul_destroy(nttmul_ctx *ctx) {
       if (L.s) (void)hipStreamDestroy(L.s);
     }
     if (d.lanes_in) (void)hipEventDestroy(d.lanes_in);
+    if (d.prod_ev) (void)hipEventDestroy(d.prod_ev);
     for (void *p : {d.fw, d.iw, (void *)d.flag})
       if (p) (void)hipFree(p);
     if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -755,9 +770,7 @@ int nttmul_kernel_name_batch(const nttmul_ctx *ctx, int word_bits, size_t batch,
   if (!ctx || (word_bits != 32 && word_bits != 64) || (cap && !buf)) return NTTMUL_EINVAL;
   if (word_bits == 32 && ctx->plan.q > 0xFFFFFFFFull) return NTTMUL_EINVAL;
   std::string name;
-  DeviceGuard guard;  // the launch choice reads the device's CU count
-  if (hipSetDevice(ctx->dev[0].id) != hipSuccess ||
-      describe_polymul(tables_for(ctx, ctx->dev[0]), word_bits, batch, &name) != hipSuccess)
+  if (describe_polymul(tables_for(ctx, ctx->dev[0]), word_bits, batch, &name) != hipSuccess)
     return NTTMUL_EUNSUPPORTED;
   if (cap) {
     const size_t k = std::min(cap - 1, name.size());
