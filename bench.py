@@ -531,7 +531,7 @@ def main(argv=None):
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": traffic_source,
-                         "kernel": ctx.kernel_name(wb, count),
+                         "kernel": ctx.last_kernel_name() or ctx.kernel_name(wb, count),
                          "kernel_ms": kern_ms,
                          "alg_bytes_per_launch": alg_bytes,
                          "buffer_sets": rotate,

@@ -92,6 +92,10 @@ int nttmul_get_info(const nttmul_ctx *ctx, nttmul_info *info);
 int nttmul_kernel_name(const nttmul_ctx *ctx, int word_bits, char *buf, size_t cap);
 int nttmul_kernel_name_batch(const nttmul_ctx *ctx, int word_bits, size_t batch, char *buf,
                              size_t cap);
+/* The kernel(s) the context's last product launch ran (same format; "" before the first one):
+ * also reflects choices made per call, e.g. the issue-prioritised variant left off when
+ * consecutive calls alternate over streams. */
+int nttmul_last_kernel_name(const nttmul_ctx *ctx, char *buf, size_t cap);
 /* Diagnostics: how the last host-buffer call on ctx moved its first chunk: 0 staged through
  * pinned buffers, 1 direct DMA from / to page-locked caller memory, 2 zero-copy kernel access to
  * the pinned staging buffers; -1 before any call. */

@@ -1461,9 +1461,9 @@ static KParams<A> product_params(const LaunchTables &T) {
 // waves per SIMD (n = 1024 x 8192, 4096 x 2048) or many generations (C3, 1024 x 262144) the
 // oldest-first order is 1-7 % faster (a finished wave frees its slot early, and the loads of the
 // next block overlap the others' arithmetic).  So: on when the launch has at most 4 waves per
-// SIMD of the device and no other product launch of the context may still be running on
-// another stream (T.prio_ok, nttmul.cpp run_device: two streams of C2 launches overlap, and then
-// the oldest-first order wins, 292 vs 262 M/s); NTTMUL_PRIO=0 / 1 forces it off / on.
+// SIMD of the device and the previous product launch of the context went to the same stream
+// (T.prio_ok, nttmul.cpp run_device: launches alternating over two streams overlap, and then the
+// oldest-first order wins, 292 vs 262 M/s at C2); NTTMUL_PRIO=0 / 1 forces it off / on.
 static thread_local int tl_prio_cus = 0;  // launch_polymul: T.cus, or 0 when T.prio_ok is 0
 static bool rows_prio(size_t waves) {
   static const int forced = [] {

@@ -25,8 +25,8 @@ struct LaunchTables {
                            // k_cols_inv); > 0 = one persistent launch (k_mp_persist) with this
                            // many steps between a polynomial's column, row and inverse tasks
   void *mp_stats = nullptr;  // tools/kbench NTTMUL_MP_STATS builds: 9 u64 task statistics
-  int prio_ok = 1;           // 0: a product launch of this context on another stream may still be
-                             // running, so k_rows keeps oldest-first issue (kernels.hip rows_prio)
+  int prio_ok = 1;           // 0: the previous product launch of this context went to another
+                             // stream, so k_rows keeps oldest-first issue (kernels.hip rows_prio)
   int pipe_per_wave = 0;     // tools/kbench builds, n = 1024, q < 2^31, u32: > 0 = k_rows_pipe with this many products
                              // per wave (loads of the next one issued before the current one's
                              // transforms); 0 = one product per one-wave workgroup (k_rows)

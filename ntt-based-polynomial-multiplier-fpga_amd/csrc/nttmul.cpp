@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <mutex>
 #include <string>
@@ -80,12 +81,12 @@ struct DevState {
   size_t slot_bytes = 0;
   int *flag = nullptr;                        // range-check result
   int cus = 0;                                // compute units (persistent grid sizing)
-  // the last fused product launch (run_device): its stream and an event after it.  A product
-  // launched on another stream while that one may still run keeps oldest-first issue
-  // (LaunchTables::prio_ok): overlapping launches are better served by it
-  std::mutex prod_mu;
-  hipEvent_t prod_ev = nullptr;
-  hipStream_t prod_s = nullptr;
+  // stream of the last fused product launch (run_device).  A product launched on another
+  // stream than the previous one keeps oldest-first issue (LaunchTables::prio_ok): launches on
+  // alternating streams overlap, and oldest-first serves overlapping launches better.  (An event
+  // query per call would say whether the previous launch still runs, but hipEventRecord +
+  // hipEventQuery cost more host time per call than a C2 launch takes: 244 -> 218 M/s.)
+  std::atomic<uintptr_t> prod_s{0};  // (uintptr_t)stream | 1 (the null stream is a stream too); 0: none
 };
 
 }  // namespace
@@ -97,6 +98,11 @@ struct nttmul_ctx {
   DevState dev[kMaxDev];
   char err[256] = {0};
   int last_path = -1;                         // run_host: 0 staged, 1 direct DMA, 2 zero-copy
+  // the last product launch (run_device, under g_err_mu): nttmul_last_kernel_name re-describes it
+  struct {
+    size_t batch = 0;
+    int io_bits = 0, prio_ok = 1, dev = -1;
+  } last_prod;
 };
 
 namespace {
@@ -267,6 +273,14 @@ int run_lanes(nttmul_ctx *ctx, DevState &d, const LaunchTables &T, const void *a
   return st;
 }
 
+void note_product(nttmul_ctx *ctx, const DevState &d, size_t batch, int io_bits, int prio_ok) {
+  std::lock_guard<std::mutex> lk(g_err_mu);
+  ctx->last_prod.batch = batch;
+  ctx->last_prod.io_bits = io_bits;
+  ctx->last_prod.prio_ok = prio_ok;
+  ctx->last_prod.dev = (int)(&d - ctx->dev);
+}
+
 // Enqueue one device-resident batch of `op` on d (current device must be d.id), using scratch sc
 // where the op needs it.  b is unused by the transforms.
 int run_device(nttmul_ctx *ctx, DevState &d, Scratch &sc, int op, void *c, const void *a,
@@ -308,12 +322,11 @@ int run_device(nttmul_ctx *ctx, DevState &d, Scratch &sc, int op, void *c, const
   const bool multipass = P.logn > 12 && op != OP_POINTWISE;
   if (!multipass && !reorder) {  // one launch over the whole batch, no scratch
     if (op == OP_MULTIPLY) {
-      std::lock_guard<std::mutex> lk(d.prod_mu);
-      if (!d.prod_ev) HIP_TRY(ctx, hipEventCreateWithFlags(&d.prod_ev, hipEventDisableTiming));
-      if (d.prod_s && d.prod_s != s && hipEventQuery(d.prod_ev) == hipErrorNotReady) T.prio_ok = 0;
+      const uintptr_t tag = (uintptr_t)s | 1;
+      const uintptr_t prev = d.prod_s.exchange(tag, std::memory_order_relaxed);
+      if (prev && prev != tag) T.prio_ok = 0;
       HIP_TRY(ctx, launch_polymul(T, a, b, c, batch, io_bits, sc.buf, s));
-      HIP_TRY(ctx, hipEventRecord(d.prod_ev, s));
-      d.prod_s = s;
+      note_product(ctx, d, batch, io_bits, T.prio_ok);
       return NTTMUL_OK;
     }
     else if (op == OP_POINTWISE) HIP_TRY(ctx, launch_pointwise(T, a, b, c, batch, io_bits, s));
@@ -360,6 +373,7 @@ int run_device(nttmul_ctx *ctx, DevState &d, Scratch &sc, int op, void *c, const
         st = fail(ctx, hipErrorLaunchFailure, "k_mp_persist: a dependency wait gave up");
     }
   }
+  if (!st && op == OP_MULTIPLY) note_product(ctx, d, chunk, io_bits, T.prio_ok);
   const int rel = scratch_release(ctx, sc, s);
   return st ? st : rel;
 }
@@ -737,7 +751,6 @@ void nttmul_destroy(nttmul_ctx *ctx) {
       if (L.s) (void)hipStreamDestroy(L.s);
     }
     if (d.lanes_in) (void)hipEventDestroy(d.lanes_in);
-    if (d.prod_ev) (void)hipEventDestroy(d.prod_ev);
     for (void *p : {d.fw, d.iw, (void *)d.flag})
       if (p) (void)hipFree(p);
     if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -781,6 +794,31 @@ int nttmul_kernel_name_batch(const nttmul_ctx *ctx, int word_bits, size_t batch,
 }
 int nttmul_kernel_name(const nttmul_ctx *ctx, int word_bits, char *buf, size_t cap) {
   return nttmul_kernel_name_batch(ctx, word_bits, 0, buf, cap);
+}
+
+int nttmul_last_kernel_name(const nttmul_ctx *ctx, char *buf, size_t cap) {
+  if (!ctx || (cap && !buf)) return NTTMUL_EINVAL;
+  size_t batch;
+  int io_bits, prio_ok, dev;
+  {
+    std::lock_guard<std::mutex> lk(g_err_mu);
+    batch = ctx->last_prod.batch;
+    io_bits = ctx->last_prod.io_bits;
+    prio_ok = ctx->last_prod.prio_ok;
+    dev = ctx->last_prod.dev;
+  }
+  std::string name;
+  if (dev >= 0) {
+    LaunchTables T = tables_for(ctx, ctx->dev[dev]);
+    T.prio_ok = prio_ok;
+    if (describe_polymul(T, io_bits, batch, &name) != hipSuccess) return NTTMUL_EUNSUPPORTED;
+  }
+  if (cap) {
+    const size_t k = std::min(cap - 1, name.size());
+    memcpy(buf, name.data(), k);
+    buf[k] = 0;
+  }
+  return (int)name.size();
 }
 
 int nttmul_multiply_batch_u32(nttmul_ctx *ctx, uint32_t *c, const uint32_t *a, const uint32_t *b,

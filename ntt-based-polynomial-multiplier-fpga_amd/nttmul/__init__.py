@@ -92,6 +92,7 @@ def load_library() -> ctypes.CDLL:
     lib.nttmul_get_info.argtypes = [vp, ctypes.POINTER(Info)]
     lib.nttmul_kernel_name.argtypes = [vp, i32, ctypes.c_char_p, sz]
     lib.nttmul_kernel_name_batch.argtypes = [vp, i32, sz, ctypes.c_char_p, sz]
+    lib.nttmul_last_kernel_name.argtypes = [vp, ctypes.c_char_p, sz]
     lib.nttmul_last_host_path.argtypes = [vp]
     for name in ("nttmul_multiply_u32", "nttmul_multiply_u64"):
         getattr(lib, name).argtypes = [vp, vp, vp, vp]
@@ -295,6 +296,14 @@ class Context:
         word_bits = word_bits or (32 if self.q < (1 << 32) else 64)
         buf = ctypes.create_string_buffer(256)
         st = self._lib.nttmul_kernel_name_batch(self._h, word_bits, batch, buf, len(buf))
+        if st < 0:
+            self._check(st)
+        return buf.value.decode()
+
+    def last_kernel_name(self) -> str:
+        """The kernel(s) the last product call launched (nttmul_last_kernel_name; "" before)."""
+        buf = ctypes.create_string_buffer(256)
+        st = self._lib.nttmul_last_kernel_name(self._h, buf, len(buf))
         if st < 0:
             self._check(st)
         return buf.value.decode()

@@ -309,6 +309,33 @@ def test_issue_priority_variants(n, q, torch_cuda):
     assert not ctx.kernel_name(32).endswith(",prio>")   # batch 0: a large batch
 
 
+def test_issue_priority_follows_streams(torch_cuda):
+    """Calls alternating over two streams overlap, so the library leaves the issue priority off
+    for them (nttmul.cpp run_device); consecutive calls on one stream get it.  The last launch is
+    named by nttmul_last_kernel_name, and the products stay exact either way."""
+    torch = torch_cuda
+    n, q, batch = 1024, Q31, 256
+    ctx = _ctx(n, q)
+    assert ctx.last_kernel_name() == ""
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    a = torch.empty(batch * n, dtype=torch.int32, device="cuda")
+    b = torch.empty_like(a)
+    c1, c2 = torch.empty_like(a), torch.empty_like(a)
+    ctx.fill_random_device(a, b, 0, batch, 32, stream=s1.cuda_stream)
+    torch.cuda.synchronize()
+    ctx.multiply_device(c1, a, b, batch, 32, stream=s1.cuda_stream)
+    assert ctx.last_kernel_name() == "k_rows<Arith32P,u32,u32,10,0,prio>"   # first call
+    ctx.multiply_device(c2, a, b, batch, 32, stream=s2.cuda_stream)
+    assert ctx.last_kernel_name() == "k_rows<Arith32P,u32,u32,10,0>"        # stream changed
+    ctx.multiply_device(c2, a, b, batch, 32, stream=s2.cuda_stream)
+    assert ctx.last_kernel_name() == "k_rows<Arith32P,u32,u32,10,0,prio>"   # same stream again
+    ctx.multiply_device(c1, a, b, batch, 32)                                 # null stream
+    assert ctx.last_kernel_name() == "k_rows<Arith32P,u32,u32,10,0>"
+    torch.cuda.synchronize()
+    assert _check_whole_batch(n, q, 32, 0, batch, a, b, c1) == batch
+    assert _check_whole_batch(n, q, 32, 0, batch, a, b, c2) == batch
+
+
 @pytest.mark.parametrize("lag", MP_LAGS)
 def test_c5_bigint_golden(golden_dir, lag, torch_cuda, monkeypatch):
     """C5 products (n = 65536, q = 0x3FFFFFFFFFE80001) on the device, through the product path the

@@ -1,7 +1,7 @@
 # Library build with the issue-prioritised k_rows variant: GPU parity suite, then kbench A/B of
 # the automatic choice against forced off / on (NTTMUL_PRIO), and the C2 / C3 bench lines
 set -o pipefail
-OUT=gpurun_out/${1:-r3_prioc2}; mkdir -p $OUT
+OUT=gpurun_out/${1:-r3_prioc4}; mkdir -p $OUT
 B=tools/kbench/bin
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || { tail -40 $OUT/gpu_tests.log; exit 1; }
 tail -2 $OUT/gpu_tests.log
@@ -16,3 +16,4 @@ run() { local name=$1; shift; timeout -k 10 240 python bench.py --no-cpu-baselin
 run c2 --n 1024 --batch-per-gpu 4096 --steps 3000 --warmup 2000
 run c3 --steps 100 --warmup 50
 run c2s --n 1024 --batch-per-gpu 4096 --steps 3000 --warmup 2000 --streams 2
+timeout -k 10 200 python -u tools/r3/c2_host_overhead.py > $OUT/host_overhead.txt 2>&1 || exit 1; tail -1 $OUT/host_overhead.txt
