@@ -335,7 +335,11 @@ int run_device(nttmul_ctx *ctx, DevState &d, Scratch &sc, int op, void *c, const
   }
   if (multipass && op == OP_MULTIPLY && env_size("NTTMUL_MP_LANES", 1) > 1) {
     const size_t chunk = sub_batch(w_poly, batch, kPipeChunkMB);
-    if (chunk < batch) return run_lanes(ctx, d, T, a, b, c, batch, chunk, io_bits, s);
+    if (chunk < batch) {
+      const int st = run_lanes(ctx, d, T, a, b, c, batch, chunk, io_bits, s);
+      if (!st) note_product(ctx, d, chunk, io_bits, T.prio_ok);
+      return st;
+    }
   }
   // sub-batches through the scratch
   const size_t chunk = sub_batch(multipass ? w_poly : io_poly, batch);

@@ -278,6 +278,8 @@ def test_full_size_device_path(n, q, word_bits, batch, chunk_mb, lanes, lag, tor
     stream = torch.cuda.current_stream().cuda_stream
     ctx.fill_random_device(a, b, 0, batch, word_bits, stream=stream)
     ctx.multiply_device(c, a, b, batch, word_bits, stream=stream)
+    # what ran is what the dry-run dispatch names for this batch (one stream: no overlap rule)
+    assert ctx.last_kernel_name() == ctx.kernel_name(word_bits, batch) != ""
     torch.cuda.synchronize()
     assert _check_whole_batch(n, q, word_bits, 0, batch, a, b, c) == batch
 
