@@ -414,7 +414,7 @@ __device__ __forceinline__ void fwd_stage(const A &ar, typename A::word (&x)[16]
 // Forward CT stages of group g on NPOLY (1 or 2) polynomials (same twiddles).  SKIP: leave out
 // the last SKIP stages of the group (the incomplete transform of the product kernel, see
 // base_mult).
-template <class A, int LOGS, int g, int NPOLY = 2, int SKIP = 0>
+template <class A, int LOGS, int g, int NPOLY = 2, int SKIP = 0, int L = 0>
 __device__ __forceinline__ void fwd_group(const A &ar, typename A::word (&x)[16],
                                           typename A::word (&y)[16],
                                           const TwPair<typename A::word> *__restrict__ tw, int j,
@@ -422,68 +422,94 @@ __device__ __forceinline__ void fwd_group(const A &ar, typename A::word (&x)[16]
                                           TwPair<typename A::word> (&zw)[16]) {
   using Gr = Groups<LOGS, kWT<A, LOGS>()>;
   constexpr int S = Gr::S(g);
+  if constexpr (sizeof(typename A::word) == 8) {
+    // 64-bit words: stages by compile-time recursion.  The loop body exceeds the unroller's
+    // threshold, and a rolled loop turns every register index into a runtime one (s_set_gpr_idx
+    // moves and per-register branches): C5 1.42 -> 1.36 ms (profiles/r3/c5/unroll_ab.txt).  (The
+    // 32-bit kernels unroll either way; the recursion reorders them for +0.2-0.8 %, so they keep
+    // the loop.)
+    if constexpr (L < S - SKIP) {
+      fwd_stage<A, LOGS, g, NPOLY, SKIP, 0>(ar, x, y, tw, j, row, l1, zw, L);
+      fwd_group<A, LOGS, g, NPOLY, SKIP, L + 1>(ar, x, y, tw, j, row, l1, zw);
+    }
+  } else {
 #pragma unroll
-  for (int l = 0; l < S - SKIP; l++) {
-    if (kWT<A, LOGS>() && g > 0 && l == 0) {  // one wave-uniform branch per group
-      if (Gr::wave_type(j))
-        fwd_stage<A, LOGS, g, NPOLY, SKIP, 1>(ar, x, y, tw, j, row, l1, zw, l);
-      else
+    for (int l = 0; l < S - SKIP; l++) {
+      if (kWT<A, LOGS>() && g > 0 && l == 0) {  // one wave-uniform branch per group
+        if (Gr::wave_type(j))
+          fwd_stage<A, LOGS, g, NPOLY, SKIP, 1>(ar, x, y, tw, j, row, l1, zw, l);
+        else
+          fwd_stage<A, LOGS, g, NPOLY, SKIP, 0>(ar, x, y, tw, j, row, l1, zw, l);
+      } else {
         fwd_stage<A, LOGS, g, NPOLY, SKIP, 0>(ar, x, y, tw, j, row, l1, zw, l);
-    } else {
-      fwd_stage<A, LOGS, g, NPOLY, SKIP, 0>(ar, x, y, tw, j, row, l1, zw, l);
+      }
     }
   }
 }
 
-// Inverse GS stages of group g (reverse stage order).  SCALE: fold F into the global stage 0.
-// SKIP: leave out the group's last SKIP forward stages (the first SKIP inverse ones).
-template <class A, int LOGS, int g, bool SCALE, int SKIP = 0>
+// One inverse GS stage l of group g.  SCALE: fold F into the global stage 0.  SKIP: the group's
+// last SKIP forward stages were left out (the first SKIP inverse ones).
+template <class A, int LOGS, int g, bool SCALE, int SKIP>
+__device__ __forceinline__ void inv_stage(const KParams<A> &P, typename A::word (&x)[16],
+                                          const TwPair<typename A::word> *__restrict__ tw, int j,
+                                          int row, int l1, int l) {
+  using Gr = Groups<LOGS, kWT<A, LOGS>()>;
+  constexpr int S = Gr::S(g), st0 = Gr::ST0(g), ns = Gr::NS(g);
+  const int dist = 8 >> l;
+  const int st = st0 + l;
+  const int tbase = (1 << (l1 + st)) + (row << st);
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    if (k & dist) continue;
+    if constexpr (A::kTyped) {
+      // first stage of the group (inverse order) reads P-type; later ones read the previous
+      // stage's Y registers (bit dist / 2 of k) as N-type; the group's last stage writes P-type
+      const bool in_n = l < S - 1 - SKIP && (k & (dist >> 1));
+      const bool out_p = l == 0;
+      if (SCALE && st == 0) {
+        if (in_n)
+          P.ar.template gs_scaled_t<true>(x[k], x[k + dist], P.f, P.fs, P.wf, P.wfs);
+        else
+          P.ar.template gs_scaled_t<false>(x[k], x[k + dist], P.f, P.fs, P.wf, P.wfs);
+        continue;
+      }
+      const int m = k / ns;
+      const int idx = tbase + (Gr::blk(g, j, k) << l) + (m >> (S - l));
+      const TwPair<typename A::word> t = out_p ? tw[idx] : tw[idx + (1 << (l1 + LOGS))];
+      if (in_n) {
+        if (out_p) P.ar.template gs_t<true, true>(x[k], x[k + dist], t.w, t.ws);
+        else P.ar.template gs_t<true, false>(x[k], x[k + dist], t.w, t.ws);
+      } else {
+        if (out_p) P.ar.template gs_t<false, true>(x[k], x[k + dist], t.w, t.ws);
+        else P.ar.template gs_t<false, false>(x[k], x[k + dist], t.w, t.ws);
+      }
+      continue;
+    }
+    if (SCALE && st == 0) {
+      P.ar.gs_scaled(x[k], x[k + dist], P.f, P.fs, P.wf, P.wfs);
+    } else {
+      const int m = k / ns;
+      const int idx = tbase + (Gr::blk(g, j, k) << l) + (m >> (S - l));
+      const TwPair<typename A::word> t = tw[NTTMUL_ABL_TWMASK ? (idx & NTTMUL_ABL_TWMASK) : idx];
+      P.ar.gs(x[k], x[k + dist], t.w, t.ws);
+    }
+  }
+}
+
+// Inverse GS stages of group g (reverse stage order); 64-bit words by compile-time recursion over
+// L (see fwd_group).
+template <class A, int LOGS, int g, bool SCALE, int SKIP = 0, int L = Groups<LOGS>::S(g) - 1 - SKIP>
 __device__ __forceinline__ void inv_group(const KParams<A> &P, typename A::word (&x)[16],
                                           const TwPair<typename A::word> *__restrict__ tw, int j,
                                           int row, int l1) {
-  using Gr = Groups<LOGS, kWT<A, LOGS>()>;
-  constexpr int S = Gr::S(g), st0 = Gr::ST0(g), ns = Gr::NS(g);
-#pragma unroll
-  for (int l = S - 1 - SKIP; l >= 0; l--) {
-    const int dist = 8 >> l;
-    const int st = st0 + l;
-    const int tbase = (1 << (l1 + st)) + (row << st);
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-      if (k & dist) continue;
-      if constexpr (A::kTyped) {
-        // first stage of the group (inverse order) reads P-type; later ones read the previous
-        // stage's Y registers (bit dist / 2 of k) as N-type; the group's last stage writes P-type
-        const bool in_n = l < S - 1 - SKIP && (k & (dist >> 1));
-        const bool out_p = l == 0;
-        if (SCALE && st == 0) {
-          if (in_n)
-            P.ar.template gs_scaled_t<true>(x[k], x[k + dist], P.f, P.fs, P.wf, P.wfs);
-          else
-            P.ar.template gs_scaled_t<false>(x[k], x[k + dist], P.f, P.fs, P.wf, P.wfs);
-          continue;
-        }
-        const int m = k / ns;
-        const int idx = tbase + (Gr::blk(g, j, k) << l) + (m >> (S - l));
-        const TwPair<typename A::word> t = out_p ? tw[idx] : tw[idx + (1 << (l1 + LOGS))];
-        if (in_n) {
-          if (out_p) P.ar.template gs_t<true, true>(x[k], x[k + dist], t.w, t.ws);
-          else P.ar.template gs_t<true, false>(x[k], x[k + dist], t.w, t.ws);
-        } else {
-          if (out_p) P.ar.template gs_t<false, true>(x[k], x[k + dist], t.w, t.ws);
-          else P.ar.template gs_t<false, false>(x[k], x[k + dist], t.w, t.ws);
-        }
-        continue;
-      }
-      if (SCALE && st == 0) {
-        P.ar.gs_scaled(x[k], x[k + dist], P.f, P.fs, P.wf, P.wfs);
-      } else {
-        const int m = k / ns;
-        const int idx = tbase + (Gr::blk(g, j, k) << l) + (m >> (S - l));
-        const TwPair<typename A::word> t = tw[NTTMUL_ABL_TWMASK ? (idx & NTTMUL_ABL_TWMASK) : idx];
-        P.ar.gs(x[k], x[k + dist], t.w, t.ws);
-      }
+  if constexpr (sizeof(typename A::word) == 8) {
+    if constexpr (L >= 0) {
+      inv_stage<A, LOGS, g, SCALE, SKIP>(P, x, tw, j, row, l1, L);
+      inv_group<A, LOGS, g, SCALE, SKIP, L - 1>(P, x, tw, j, row, l1);
     }
+  } else {
+#pragma unroll
+    for (int l = L; l >= 0; l--) inv_stage<A, LOGS, g, SCALE, SKIP>(P, x, tw, j, row, l1, l);
   }
 }
 
