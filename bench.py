@@ -52,6 +52,29 @@ def timed_steps(step, steps: int, warmup: int, sync, barrier):
     return time.perf_counter() - t0
 
 
+def settle(step, ms: float, sync, clock=time.perf_counter):
+    """Run the hot path, untimed and before the W warm-up steps, until `ms` of wall time have
+    passed, in synchronised chunks that double while a chunk takes under 10 ms (so a fast step is
+    never queued far ahead of the device).  On an idle MI355X the first ~50 ms of C3 launches run
+    8-9 % slower than the sustained rate (profiles/r3/warm/out.txt: W=0/5 K=20 58.5/61.0 M/s,
+    W=50 K=100 66.7, W=200 K=20 66.4 on one box); the driver's --warmup 5 is 5 ms at C3.
+    Returns (steps run, wall ms)."""
+    if ms <= 0:
+        return 0, 0.0
+    t0 = clock()
+    n, chunk = 0, 1
+    while True:
+        c0 = clock()
+        for _ in range(chunk):
+            step()
+        sync()
+        n += chunk
+        if (clock() - t0) * 1e3 >= ms:
+            return n, (clock() - t0) * 1e3
+        if (clock() - c0) * 1e3 < 10.0:
+            chunk *= 2
+
+
 def max_over_ranks(x: float, dist, device=None) -> float:
     """Max of a per-rank float over the (gloo) process group; identity when not distributed.
     A CPU tensor: the control plane never touches the GPUs or RCCL."""
@@ -86,6 +109,9 @@ def parse(argv=None):
                     help="alternate consecutive steps over this many HIP streams (default 1; 2 "
                          "overlaps one launch's tail with the next one's ramp: a C2-sized batch "
                          "is a single generation of workgroups)")
+    ap.add_argument("--settle-ms", type=float, default=200.0,
+                    help="before the W warm-up steps, run the hot path untimed for this long so "
+                         "the card leaves its idle clock state (reported as 'settle'; 0 disables)")
     ap.add_argument("--power-seconds", type=float, default=4.0,
                     help="after the timed region, keep stepping this long while amd-smi samples "
                          "board power and clocks (rank 0 at N=1; 0 disables)")
@@ -488,6 +514,7 @@ def main(argv=None):
                 stream.wait_event(st.record_event())
             ev1.record(stream)
 
+    settle_steps, settle_ms = settle(step, args.settle_ms, lambda: torch.cuda.synchronize(dev))
     wall = timed_steps(timed_step, args.steps, args.warmup, lambda: torch.cuda.synchronize(dev),
                        (lambda: dist.barrier()) if world > 1 else (lambda: None))
     kern_ms = ev0.elapsed_time(ev1) / args.steps
@@ -516,6 +543,9 @@ def main(argv=None):
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle": {"steps": settle_steps, "ms": round(settle_ms, 1),
+                       "note": "untimed hot-path steps before the W warm-up steps, so the card "
+                               "is past its idle clock ramp (DESIGN.md §5 'Run length')"},
             "ms_per_step": wall_max / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "weak",

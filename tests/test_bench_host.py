@@ -158,3 +158,21 @@ def test_weak_scaling_batch_is_constant():
     """--batch-per-gpu is the same at every N (no switch to C4's slice at 8 ranks)."""
     assert bench.parse([]).batch_per_gpu == 65536
     assert bench.parse(["--gpus", "8"]).batch_per_gpu == 65536
+
+
+def test_settle_runs_untimed_chunks_until_the_wall_time():
+    """bench.settle: synchronised chunks doubling while under 10 ms, stopping once `ms` passed."""
+    t = {"now": 0.0, "steps": 0, "syncs": 0}
+
+    def step():
+        t["steps"] += 1
+        t["now"] += 1e-3          # each step costs 1 ms of (fake) wall time
+
+    def sync():
+        t["syncs"] += 1
+
+    n, ms = bench.settle(step, 100.0, sync, clock=lambda: t["now"])
+    assert n == t["steps"] and ms >= 100.0
+    assert n < 200                # chunks stop doubling at 10 ms, so little overshoot
+    assert t["syncs"] >= 5        # paced: never one unsynchronised burst
+    assert bench.settle(step, 0, sync) == (0, 0.0)
