@@ -286,9 +286,9 @@ void note_product(nttmul_ctx *ctx, const DevState &d, size_t batch, int io_bits,
 int run_device(nttmul_ctx *ctx, DevState &d, Scratch &sc, int op, void *c, const void *a,
                const void *b, size_t batch, int io_bits, hipStream_t s) {
   const Plan &P = ctx->plan;
-  if (!batch) return NTTMUL_OK;
   if (io_bits != 32 && io_bits != 64) return NTTMUL_EINVAL;
   if (io_bits == 32 && P.q > 0xFFFFFFFFull) return NTTMUL_EINVAL;  // q does not fit the words
+  if (!batch) return NTTMUL_OK;  // an empty batch: nothing enqueued, no pointer dereferenced
   if (ctx->flags & NTTMUL_FLAG_VALIDATE) {
     HIP_TRY(ctx, hipMemsetAsync(d.flag, 0, sizeof(int), s));
     HIP_TRY(ctx, launch_check_range(a, (op == OP_MULTIPLY || op == OP_POINTWISE) ? b : a, P.q,
@@ -592,8 +592,10 @@ int run_host_dev(nttmul_ctx *ctx, DevState &d, const HostJob &J, size_t p0, size
 int run_host(nttmul_ctx *ctx, int op, void *c, const void *a, const void *b, size_t batch,
              int io_bits) {
   const bool two = op == OP_MULTIPLY || op == OP_POINTWISE;
-  if (!ctx || !c || !a || (two && !b)) return NTTMUL_EINVAL;
+  // pointers may be null for an empty batch, as on the device path (device_op)
+  if (!ctx || (batch && (!c || !a || (two && !b)))) return NTTMUL_EINVAL;
   if (io_bits != 32 && io_bits != 64) return NTTMUL_EINVAL;
+  if (io_bits == 32 && ctx->plan.q > 0xFFFFFFFFull) return NTTMUL_EINVAL;
   if (!batch) return NTTMUL_OK;
   DeviceGuard guard;
   HostJob J;

@@ -424,6 +424,38 @@ def test_validate_flag(torch_cuda):
     assert ei.value.status == nttmul.NTTMUL_ERANGE
 
 
+def test_empty_and_invalid_calls(torch_cuda):
+    """Edge cases of the product entry points: an empty batch is a successful no-op on both paths
+    (null pointers allowed, nothing written), a non-empty batch with a null operand, a word size
+    other than 32/64 or 32-bit words for a 62-bit q are NTTMUL_EINVAL, on the host path as on the
+    device path."""
+    import ctypes
+    lib = nttmul.load_library()
+    ctx = _ctx(1024, Q31)
+    h = ctx._h
+    md = lib.nttmul_multiply_batch_device
+    s = torch_cuda.cuda.current_stream().cuda_stream
+    c = torch_cuda.full((1024,), 7, dtype=torch_cuda.int32, device="cuda")
+    assert md(h, None, None, None, 0, 32, 0, ctypes.c_void_p(s)) == nttmul.NTTMUL_OK
+    assert md(h, c.data_ptr(), c.data_ptr(), c.data_ptr(), 0, 32, 0, ctypes.c_void_p(s)) == 0
+    torch_cuda.cuda.synchronize()
+    assert bool((c == 7).all())                                   # nothing written
+    assert md(h, None, c.data_ptr(), c.data_ptr(), 1, 32, 0, None) == nttmul.NTTMUL_EINVAL
+    assert md(h, c.data_ptr(), c.data_ptr(), c.data_ptr(), 0, 7, 0, None) == nttmul.NTTMUL_EINVAL
+    mh = lib.nttmul_multiply_batch_u32
+    assert mh(h, None, None, None, 0) == nttmul.NTTMUL_OK
+    buf = np.zeros(1024, dtype=np.uint32)
+    assert mh(h, buf.ctypes.data, None, buf.ctypes.data, 1) == nttmul.NTTMUL_EINVAL
+    out = ctx.multiply(np.zeros((0, 1024), np.uint32), np.zeros((0, 1024), np.uint32))
+    assert out.shape == (0, 1024)
+    c62 = _ctx(1024, Q62)
+    for bt in (0, 1):    # 32-bit words cannot hold a 62-bit q's residues, empty batch or not
+        assert lib.nttmul_multiply_batch_u32(c62._h, buf.ctypes.data, buf.ctypes.data,
+                                             buf.ctypes.data, bt) == nttmul.NTTMUL_EINVAL
+        assert md(c62._h, c.data_ptr(), c.data_ptr(), c.data_ptr(), bt, 32, 0,
+                  None) == nttmul.NTTMUL_EINVAL
+
+
 def test_single_multiply_entry(torch_cuda):
     a, b = O.fill_inputs(4096, Q31, 3, 1)
     c = nttmul.multiply(a[0], b[0], 4096, Q31)
