@@ -9,7 +9,7 @@ global batch and no input crosses PCIe or xGMI).  Scaling is weak: each GPU mult
 path and no RCCL at all: torch.distributed runs on gloo over CPU tensors and provides only the
 barrier and the max-over-ranks time.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 4096] [--q 2013265921]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--settle-ms 200] [--n 4096] [--q 2013265921]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
 Prints ONE JSON line on rank 0 (fields documented in DESIGN.md §Measurement).
@@ -55,9 +55,10 @@ def timed_steps(step, steps: int, warmup: int, sync, barrier):
 def settle(step, ms: float, sync, clock=time.perf_counter):
     """Run the hot path, untimed and before the W warm-up steps, until `ms` of wall time have
     passed, in synchronised chunks that double while a chunk takes under 10 ms (so a fast step is
-    never queued far ahead of the device).  On an idle MI355X the first ~50 ms of C3 launches run
-    8-9 % slower than the sustained rate (profiles/r3/warm/out.txt: W=0/5 K=20 58.5/61.0 M/s,
-    W=50 K=100 66.7, W=200 K=20 66.4 on one box); the driver's --warmup 5 is 5 ms at C3.
+    never queued far ahead of the device).  On an idle MI355X the first ~40 ms of C3 launches run
+    slower than the sustained rate (profiles/r3/warm/ramp.txt: launches 0-4 1.22 ms, 10-19 1.07,
+    from 40 ms on 0.986; out.txt: W=0/5 K=20 58.5/61.0 M/s, W=50 K=100 66.7, W=200 K=20 66.4 on
+    one box); the driver's --warmup 5 is 5 ms at C3.
     Returns (steps run, wall ms)."""
     if ms <= 0:
         return 0, 0.0
@@ -545,7 +546,7 @@ def main(argv=None):
             "warmup": args.warmup,
             "settle": {"steps": settle_steps, "ms": round(settle_ms, 1),
                        "note": "untimed hot-path steps before the W warm-up steps, so the card "
-                               "is past its idle clock ramp (DESIGN.md §5 'Run length')"},
+                               "is past its idle clock ramp (DESIGN.md §5 'Settle phase')"},
             "ms_per_step": wall_max / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
