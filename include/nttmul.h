@@ -111,7 +111,9 @@ int nttmul_multiply_u64(nttmul_ctx *ctx, uint64_t *c, const uint64_t *a, const u
  * through the context's pinned buffers by host threads (the bound of this path); when a, b and c
  * all lie in page-locked memory (nttmul_host_alloc, or hipHostMalloc / hipHostRegister by the
  * caller) the copy engines DMA the chunks straight from and to them, as the FPGA communicator's
- * PCIE_DmaWrite / PCIE_DmaRead did from its own buffers (NTT_PCIECommunicationv2.c:164-229). */
+ * PCIE_DmaWrite / PCIE_DmaRead did from its own buffers (NTT_PCIECommunicationv2.c:164-229).
+ * batch = 0 is a successful no-op (the pointers may then be NULL; here and on the device path);
+ * a NULL operand with batch > 0, or 32-bit words for a q >= 2^32, is NTTMUL_EINVAL. */
 int nttmul_multiply_batch_u32(nttmul_ctx *ctx, uint32_t *c, const uint32_t *a, const uint32_t *b,
                               size_t batch);
 int nttmul_multiply_batch_u64(nttmul_ctx *ctx, uint64_t *c, const uint64_t *a, const uint64_t *b,
