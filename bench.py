@@ -116,6 +116,10 @@ def parse(argv=None):
     ap.add_argument("--power-seconds", type=float, default=4.0,
                     help="after the timed region, keep stepping this long while amd-smi samples "
                          "board power and clocks (rank 0 at N=1; 0 disables)")
+    ap.add_argument("--clock-seconds", type=float, default=2.0,
+                    help="after the power probe, run the same product from the diagnostic build "
+                         "lib/libnttmul_diag.so this long and report the in-kernel clock "
+                         "(rank 0 at N=1; 0 disables)")
     ap.add_argument("--dump-samples", default="",
                     help="write <prefix>.rank<r>.npz with sampled products of this rank's slice "
                          "(checked against the oracle by tests/test_gpu_parity.py)")
@@ -441,6 +445,59 @@ def power_probe(step, sync, seconds: float, reader, units_per_step: int = 0):
     return out
 
 
+def diag_clock(n: int, q: int, wb: int, count: int, a, b, c, devno: int, stream_ptr: int,
+               sync, seconds: float = 2.0):
+    """The shader clock the product kernel holds, read inside the kernel (MI355X_MICROARCH.md
+    'DVFS give-back' item 6): the same product runs from lib/libnttmul_diag.so -- the production
+    kernels plus s_memtime / s_memrealtime stamps by thread 0 of each k_rows workgroup
+    (include/nttmul_diag.h) -- back to back for `seconds` on the bench's device-resident inputs,
+    then the last launch's per-workgroup clocks d(memtime) / d(realtime) x 100 MHz are summarised
+    (median over workgroups).  None when the diagnostic library is not built."""
+    import ctypes
+    import statistics
+    import time as _t
+    import numpy as np
+    import nttmul
+    try:
+        lib = nttmul.load_diag_library()
+    except ImportError:
+        return None
+    ctx = nttmul.Context(n, q, ndev=1, first_dev=devno, _lib=lib)
+    try:
+        t0 = _t.perf_counter()
+        launches = 0
+        while _t.perf_counter() - t0 < seconds:
+            for _ in range(16):
+                ctx.multiply_device(c, a, b, count, wb, stream=stream_ptr)
+            sync()
+            launches += 16
+        # k_rows workgroups of that launch (products per workgroup: 256 / (n / 16) threads,
+        # one 64-thread workgroup per product at n = 1024; n > 4096: 2^(logn - 12) rows each)
+        logn = n.bit_length() - 1
+        units = count << max(0, logn - 12)
+        per_wg = 1 if logn >= 10 else 256 // (n // 16)
+        wgs = min(-(-units // per_wg), 1 << 16)
+        st = np.zeros(wgs * 4, dtype=np.uint64)
+        if lib.nttmul_diag_clock_stamps(st.ctypes.data, wgs) != 0:
+            return {"error": "nttmul_diag_clock_stamps failed"}
+        st = st.reshape(wgs, 4).astype(np.float64)
+        dr = st[:, 3] - st[:, 1]
+        ok = dr > 0
+        mhz = ((st[ok, 2] - st[ok, 0]) / dr[ok] * 100.0).tolist()
+        if not mhz:
+            return {"error": "no stamps"}
+        mhz.sort()
+        return {"clock_ghz_median": statistics.median(mhz) / 1e3,
+                "clock_ghz_p10": mhz[len(mhz) // 10] / 1e3, "clock_ghz_p90": mhz[len(mhz) * 9 // 10] / 1e3,
+                "workgroups": len(mhz), "launches_before": launches,
+                "kernel": ctx.last_kernel_name(),
+                "source": "lib/libnttmul_diag.so (production kernels + clock stamps), "
+                          f"{launches} launches back to back on the bench inputs, then the last "
+                          "launch's per-workgroup d(s_memtime) / d(s_memrealtime) x 100 MHz"}
+    finally:
+        ctx.close()
+
+
 MAX_CLOCK_GHZ = 2.4         # MI355X max engine clock (MI355X_MICROARCH.md)
 SIMDS = 1024                # 256 CUs x 4 SIMDs
 
@@ -606,6 +663,21 @@ def main(argv=None):
                                             units_per_step=count)
             except Exception as e:  # reported evidence, never required
                 line["power"] = {"error": str(e)}
+        if world == 1 and args.clock_seconds > 0:
+            a, b, c = sets[0]
+            try:
+                clk = diag_clock(n, q, wb, count, a, b, c, devno, sptr,
+                                 lambda: torch.cuda.synchronize(dev), args.clock_seconds)
+            except Exception as e:  # reported evidence, never required
+                clk = {"error": str(e)}
+            if clk:
+                line["in_kernel_clock"] = clk
+                vr = line.get("valu_roofline")
+                if vr and clk.get("clock_ghz_median"):  # the issue bound at the clock actually held
+                    g = clk["clock_ghz_median"]
+                    vr["in_kernel_clock_ghz"] = g
+                    vr["bound_ms_at_in_kernel_clock"] = vr["cycles_per_wave"] * vr["waves_per_simd"] / (g * 1e9) * 1e3
+                    vr["frac_at_in_kernel_clock"] = vr["bound_ms_at_in_kernel_clock"] / kern_ms
         if args.host_io:
             a, b, _ = sets[0]
             line["host_io"] = host_io(ctx, a, b, count, n, wb)

@@ -62,6 +62,18 @@ typedef struct {
                           own host thread; <= 0 = all visible devices                           */
   int first_dev;       /* first HIP device index used                                           */
   uint32_t flags;      /* NTTMUL_FLAG_*                                                          */
+  /* Dispatch and runtime knobs, read once by nttmul_create_ex (0 = the default in brackets; a
+   * zero-initialised struct gets every default).  The library reads no environment variable. */
+  int32_t issue_prio;   /* fused products (n <= 4096, q < 2^31): 0 = automatic [the issue-
+                           prioritised kernel for launches of at most 4 waves per SIMD made on the
+                           same stream as the context's previous product launch], 1 = always,
+                           -1 = never (oldest-first issue)                                       */
+  int32_t zero_copy_kb; /* host-buffer calls, n <= 4096: per-operand chunks up to this many KiB
+                           run zero-copy on the pinned staging buffers [64]; -1 = never          */
+  int32_t copy_threads; /* host threads splitting each large staging copy [8], capped at the
+                           host's hardware threads                                              */
+  uint32_t scratch_mb;  /* n > 4096 products and reordered transforms: at most this many MiB per
+                           scratch buffer; larger batches run in sub-batches through it [512]   */
 } nttmul_params;
 
 typedef struct {

@@ -742,6 +742,34 @@ __device__ __forceinline__ unsigned wave_slot() {
 #define WTRACE(k) do { } while (0)
 #endif
 
+// In-kernel clock (lib/libnttmul_diag.so only, built with NTTMUL_CLOCK_STAMPS; MI355X_MICROARCH.md
+// 'DVFS give-back' item 6): thread 0 of each k_rows workgroup stamps s_memtime (shader clock) and
+// s_memrealtime (100 MHz) at entry and after issuing its stores, into a buffer of its own that no
+// other code reads; the workgroup's clock is d(memtime) / d(realtime) x 100 MHz.  The product
+// kernels of libnttmul.so execute no stamp.
+#ifdef NTTMUL_CLOCK_STAMPS
+constexpr unsigned kClkSlots = 1u << 16;
+__device__ unsigned long long g_clk[kClkSlots * 4];
+hipError_t read_clock_stamps(void *dst, size_t blocks) {
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_clk),
+                             (blocks < kClkSlots ? blocks : kClkSlots) * 4 * sizeof(unsigned long long));
+}
+__device__ __forceinline__ void clk_stamp(int k) {
+  if (threadIdx.x == 0) {
+    unsigned long long t, r;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(t), "=s"(r)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    unsigned long long *p = g_clk + (blockIdx.x % kClkSlots) * 4 + 2 * k;
+    p[0] = t;
+    p[1] = r;
+  }
+}
+#define CLK_STAMP(k) clk_stamp(k)
+#else
+#define CLK_STAMP(k) do { } while (0)
+#endif
+
 template <class A, class TIn, class TOut, int LOGS, int L1, bool PRIO = false>
 __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
     KParams<A> P, const TIn *__restrict__ a, const TIn *__restrict__ b, TOut *__restrict__ c,
@@ -767,6 +795,7 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
 #endif
 
   WTRACE(0);
+  CLK_STAMP(0);
   if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);  // rows_prio
 #ifdef NTTMUL_STAGGER  // kbench experiment: one-wave blocks of generation blockIdx / 1024 wait
   if constexpr (LOGS == 10 && L1 == 0)
@@ -855,6 +884,7 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
       WTRACE(3);
 #endif
     }
+    CLK_STAMP(1);
     return;
   }
   if (live) {
@@ -865,6 +895,7 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
       st_stream<kNT>(c + base_g + Gr::off(0, k), (TOut)v);
     }
   }
+  CLK_STAMP(1);
 }
 
 // C2 in-launch overlap experiments (tools/kbench builds only: both measured slower
@@ -1176,8 +1207,12 @@ __global__ __launch_bounds__(256) void k_cols_inv(KParams<A> P,
 }
 
 // ---------------------------------------------------------------------------------------------
-// Persistent, phase-pipelined multi-pass product (n = 2^L1 * 4096 > 4096)
+// Persistent, phase-pipelined multi-pass product (n = 2^L1 * 4096 > 4096) -- tools/kbench builds
+// only: measured slower than the three launches (profiles/r3/c5_persist/), so the
+// library does not carry it (round 4: no product path of libnttmul.so can return after a
+// given-up dependency wait)
 // ---------------------------------------------------------------------------------------------
+#ifdef NTTMUL_KBENCH_BUILD
 // The three passes of multipass_l1 (k_cols_fwd -> k_rows<..., 12, L1> -> k_cols_inv) as tasks of
 // ONE launch: a grid of resident workgroups pulls tickets from a device-side counter.  Per
 // polynomial p there are kMpCols column-forward tasks CF(p, s) (256 columns each, all 2^L1
@@ -1388,6 +1423,8 @@ __global__ __launch_bounds__(256) void k_mp_persist(KParams<A> P, const IO *__re
   }
 }
 
+#endif  // NTTMUL_KBENCH_BUILD
+
 // ---------------------------------------------------------------------------------------------
 // Synthetic inputs and input validation
 // ---------------------------------------------------------------------------------------------
@@ -1489,14 +1526,12 @@ static KParams<A> product_params(const LaunchTables &T) {
 // next block overlap the others' arithmetic).  So: on when the launch has at most 4 waves per
 // SIMD of the device and the previous product launch of the context went to the same stream
 // (T.prio_ok, nttmul.cpp run_device: launches alternating over two streams overlap, and then the
-// oldest-first order wins, 292 vs 262 M/s at C2); NTTMUL_PRIO=0 / 1 forces it off / on.
-static thread_local int tl_prio_cus = 0;  // launch_polymul: T.cus, or 0 when T.prio_ok is 0
+// oldest-first order wins, 292 vs 262 M/s at C2); nttmul_params.issue_prio -1 / 1 forces it off /
+// on for a context.
+static thread_local int tl_prio_cus = 0;   // launch_polymul: T.cus, or 0 when T.prio_ok is 0
+static thread_local int tl_prio_mode = 0;  // launch_polymul: T.prio (nttmul_params.issue_prio)
 static bool rows_prio(size_t waves) {
-  static const int forced = [] {
-    const char *e = getenv("NTTMUL_PRIO");
-    return e && *e ? atoi(e) : -1;
-  }();
-  if (forced >= 0) return forced > 0;
+  if (tl_prio_mode) return tl_prio_mode > 0;
   return waves <= (size_t)tl_prio_cus * 4 * 4;  // 4 SIMDs per CU, 4 waves per SIMD
 }
 
@@ -1615,6 +1650,7 @@ static hipError_t multipass_l1(const LaunchTables &T, const void *a, const void 
   return hipGetLastError();
 }
 
+#ifdef NTTMUL_KBENCH_BUILD
 // The same product as multipass_l1 in one persistent launch (k_mp_persist).  scr[3]: the
 // ticket / counter words, mp_sync_bytes(batch), zeroed here on the stream before the launch.
 template <class A, class IO, int L1>
@@ -1628,12 +1664,12 @@ static hipError_t multipass_persist(const LaunchTables &T, const void *a, const 
   }
   if (batch == 0) return hipSuccess;
   if (batch > 0x7FFFFFFFull / (2 * kMpCols + (1 << L1))) return hipErrorInvalidValue;
-  static int per_cu = 0;  // resident workgroups per CU (occupancy of this instantiation)
-  if (!per_cu) {
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, reinterpret_cast<const void *>(&k_mp_persist<A, IO, L1>), 256, 0);
-    if (e != hipSuccess || per_cu < 1) per_cu = 1;
-  }
+  static const int per_cu = [] {  // resident workgroups per CU (occupancy of this instantiation)
+    int k = 0;
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &k, reinterpret_cast<const void *>(&k_mp_persist<A, IO, L1>), 256, 0);
+    return e != hipSuccess || k < 1 ? 1 : k;
+  }();
   const KParams<A> P = product_params<A>(T);
   unsigned *sw = (unsigned *)scr[3];
   hipError_t e = hipMemsetAsync(sw, 0, mp_sync_bytes(batch), s);
@@ -1651,9 +1687,12 @@ static hipError_t multipass_persist(const LaunchTables &T, const void *a, const 
   return hipGetLastError();
 }
 
+#endif  // NTTMUL_KBENCH_BUILD
+
 template <class A, class IO>
 static hipError_t multipass(const LaunchTables &T, const void *a, const void *b, void *c,
                             size_t batch, void **scr, hipStream_t s) {
+#ifdef NTTMUL_KBENCH_BUILD
   if (T.mp_lag > 0 && scr[3] && !(T.logn == 16 && NTTMUL_SPLIT16 == 5)) {
     switch (T.logn) {
       case 13: return multipass_persist<A, IO, 1>(T, a, b, c, batch, scr, s);
@@ -1663,6 +1702,7 @@ static hipError_t multipass(const LaunchTables &T, const void *a, const void *b,
       default: return hipErrorInvalidValue;
     }
   }
+#endif
   switch (T.logn) {
     case 13: return multipass_l1<A, IO, 1>(T, a, b, c, batch, scr[0], scr[1], scr[2], s);
     case 14: return multipass_l1<A, IO, 2>(T, a, b, c, batch, scr[0], scr[1], scr[2], s);
@@ -1697,10 +1737,12 @@ static hipError_t launch_polymul_(const LaunchTables &T, const void *a, const vo
                                   size_t batch, int io_bits, void **scr, hipStream_t s);
 hipError_t launch_polymul(const LaunchTables &T, const void *a, const void *b, void *c,
                           size_t batch, int io_bits, void **scr, hipStream_t s) {
-  const int prev = tl_prio_cus;
+  const int prev = tl_prio_cus, prev_mode = tl_prio_mode;
   tl_prio_cus = T.prio_ok ? T.cus : 0;
+  tl_prio_mode = T.prio;
   const hipError_t e = launch_polymul_(T, a, b, c, batch, io_bits, scr, s);
   tl_prio_cus = prev;
+  tl_prio_mode = prev_mode;
   return e;
 }
 static hipError_t launch_polymul_(const LaunchTables &T, const void *a, const void *b, void *c,
@@ -1734,7 +1776,7 @@ static hipError_t launch_polymul_(const LaunchTables &T, const void *a, const vo
 
 hipError_t describe_polymul(const LaunchTables &T, int io_bits, size_t batch, std::string *out) {
   out->clear();
-  void *scr[4] = {nullptr, nullptr, nullptr, (void *)out};  // (non-null: the persistent form)
+  void *scr[4] = {nullptr, nullptr, nullptr, (void *)out};  // (kbench: non-null = persistent form)
   tl_describe = out;
   const hipError_t e = launch_polymul(T, nullptr, nullptr, nullptr, batch ? batch : (size_t)1 << 24,
                                       io_bits, scr, nullptr);

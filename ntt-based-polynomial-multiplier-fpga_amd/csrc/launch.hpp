@@ -20,24 +20,27 @@ struct LaunchTables {
   uint64_t r2;             // R^2 mod q (standalone pointwise product)
   const void *fw, *iw;     // forward / inverse twiddle (value, companion) pairs, n entries
                            // (planner.cpp tw_pair: Shoup, or Montgomery form for Arith32)
-  int cus;                 // compute units of the device (persistent grid size)
-  int mp_lag;              // n > 4096: 0 = three launches per product (k_cols_fwd, k_rows,
-                           // k_cols_inv); > 0 = one persistent launch (k_mp_persist) with this
-                           // many steps between a polynomial's column, row and inverse tasks
-  void *mp_stats = nullptr;  // tools/kbench NTTMUL_MP_STATS builds: 9 u64 task statistics
-  int prio_ok = 1;           // 0: the previous product launch of this context went to another
-                             // stream, so k_rows keeps oldest-first issue (kernels.hip rows_prio)
+  int cus;                 // compute units of the device (launch-shape thresholds)
+  int prio = 0;            // nttmul_params.issue_prio: -1 never, 0 automatic, 1 always
+  int prio_ok = 1;         // 0: the previous product launch of this context went to another
+                           // stream, so automatic mode keeps oldest-first issue (kernels.hip rows_prio)
+  // tools/kbench builds only (the library never sets them):
+  int mp_lag = 0;            // n > 4096: > 0 = one persistent launch (k_mp_persist) with this
+                             // many steps between a polynomial's column, row and inverse tasks
+  void *mp_stats = nullptr;  // NTTMUL_MP_STATS builds: 9 u64 task statistics
   int pipe_per_wave = 0;     // tools/kbench builds, n = 1024, q < 2^31, u32: > 0 = k_rows_pipe with this many products
                              // per wave (loads of the next one issued before the current one's
                              // transforms); 0 = one product per one-wave workgroup (k_rows)
 };
 
+#ifdef NTTMUL_KBENCH_BUILD
 // Bytes of the ticket / counter words k_mp_persist needs for `batch` polynomials (scr[3]).
 inline size_t mp_sync_bytes(size_t batch) { return (2 * batch + 2) * sizeof(unsigned); }
+#endif
 
 // c = a * b for `batch` polynomials of n = 2^logn words of io_bits (32/64) each, on stream s.
-// scr: three device buffers of batch * n words of word_bits, used only when n > 4096, and a
-// fourth of mp_sync_bytes(batch) for the persistent form (T.mp_lag > 0; nullptr: three launches).
+// scr: three device buffers of batch * n words of word_bits, used only when n > 4096 (kbench
+// builds: a fourth of mp_sync_bytes(batch) for the persistent form, T.mp_lag > 0).
 hipError_t launch_polymul(const LaunchTables &T, const void *a, const void *b, void *c,
                           size_t batch, int io_bits, void **scr, hipStream_t s);
 // The kernels launch_polymul would launch for (T, io_bits), as "k_rows<Arith32P3,u32,u32,12,0>"
@@ -55,6 +58,11 @@ hipError_t launch_bitrev(const void *in, void *out, uint32_t logn, size_t batch,
                          hipStream_t s);
 hipError_t launch_fill(void *a, void *b, uint32_t logn, uint64_t q, uint64_t seed, uint64_t p0,
                        size_t count, int io_bits, hipStream_t s);
+#ifdef NTTMUL_CLOCK_STAMPS
+// lib/libnttmul_diag.so: the k_rows clock stamps of the last launch, 4 u64 per workgroup
+// (entry memtime, entry realtime, end memtime, end realtime), workgroups 0 .. blocks - 1
+hipError_t read_clock_stamps(void *dst, size_t blocks);
+#endif
 hipError_t launch_check_range(const void *a, const void *b, uint64_t q, size_t total, int io_bits,
                               int *bad, hipStream_t s);
 

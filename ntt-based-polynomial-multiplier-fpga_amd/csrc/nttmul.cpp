@@ -26,9 +26,6 @@
 #include "launch.hpp"
 #include "nttmul.h"
 
-#ifndef NTTMUL_MP_LAG_DEFAULT
-#define NTTMUL_MP_LAG_DEFAULT 0
-#endif
 #include "planner.hpp"
 
 using namespace nttmul;
@@ -40,14 +37,13 @@ constexpr int kSlots = 3;                     // host-path pipeline depth per de
 constexpr size_t kChunkBytes = 8u << 20;      // host-path chunk, per operand
 
 // Multi-pass scratch (n > 4096: the column/row intermediates) and the bit-reversed copy of a
-// reordered transform's input.  Sized for a sub-batch of mp_chunk polynomials, not the whole
-// batch, so the intermediates of one sub-batch stay in the 256 MiB Infinity Cache between the
-// column and row passes.  Every use is ordered after the previous one by `ev`, whatever stream
-// it was enqueued on: two device-API calls on different streams (or two host-path slots) never
-// overwrite each other's intermediates.
+// reordered transform's input, sized for a sub-batch of at most params.scratch_mb per buffer.
+// Every use is ordered after the previous one by `ev`, whatever stream it was enqueued on: two
+// device-API calls on different streams (or two host-path slots) never overwrite each other's
+// intermediates.
 struct Scratch {
-  void *buf[4] = {nullptr, nullptr, nullptr, nullptr};  // [3]: k_mp_persist's ticket words
-  size_t bytes = 0, sync_bytes = 0;
+  void *buf[3] = {nullptr, nullptr, nullptr};
+  size_t bytes = 0;
   void *perm = nullptr;
   size_t perm_bytes = 0;
   hipEvent_t ev = nullptr;                    // recorded after the last enqueued use
@@ -55,22 +51,11 @@ struct Scratch {
   hipStream_t last = nullptr;                 // stream of that use
 };
 
-// One lane of the pipelined multi-pass product: an internal stream and its own scratch.
-// Sub-batches alternate over kLanes lanes, so one sub-batch's HBM-bound column passes run beside
-// another's VALU-bound row pass.
-constexpr int kLanes = 2;
-struct Lane {
-  hipStream_t s = nullptr;
-  Scratch sc;
-};
-
 struct DevState {
   int id = -1;
   hipStream_t stream = nullptr;
   void *fw = nullptr, *iw = nullptr;
   Scratch dscr;                               // device-resident API calls
-  Lane lane[kLanes];                          // pipelined multi-pass products
-  hipEvent_t lanes_in = nullptr;              // the caller's stream reached the product
   // host-buffer path: kSlots pipeline slots, each with a stream, pinned host staging, device
   // buffers for a, b, c and its own scratch (run_host)
   hipStream_t xs[kSlots] = {};
@@ -97,6 +82,11 @@ struct nttmul_ctx {
   int ndev = 0;
   DevState dev[kMaxDev];
   char err[256] = {0};
+  // nttmul_params knobs, fixed at create (include/nttmul.h)
+  int issue_prio = 0;                         // -1 never, 0 automatic, 1 always
+  size_t zero_copy = 64u << 10;               // per-operand bytes run zero-copy (0: never)
+  unsigned copy_threads = 8;
+  size_t scratch_bytes = (size_t)512 << 20;   // per scratch buffer
   int last_path = -1;                         // run_host: 0 staged, 1 direct DMA, 2 zero-copy
   // the last product launch (run_device, under g_err_mu): nttmul_last_kernel_name re-describes it
   struct {
@@ -133,15 +123,6 @@ int fail(nttmul_ctx *ctx, hipError_t e, const char *what) {
     if (_e != hipSuccess) return fail(ctx, _e, #expr); \
   } while (0)
 
-// n > 4096 products: NTTMUL_MP_LAG > 0 runs the three passes as one persistent launch
-// (kernels.hip k_mp_persist) with that many steps between a polynomial's column, row and inverse
-// tasks; 0 = three launches.  Default kMpLagDefault.
-constexpr int kMpLagDefault = NTTMUL_MP_LAG_DEFAULT;
-int mp_lag() {
-  const char *e = getenv("NTTMUL_MP_LAG");
-  return e ? std::max(0, atoi(e)) : kMpLagDefault;
-}
-
 LaunchTables tables_for(const nttmul_ctx *ctx, const DevState &d) {
   const Plan &P = ctx->plan;
   LaunchTables T;
@@ -156,7 +137,7 @@ LaunchTables tables_for(const nttmul_ctx *ctx, const DevState &d) {
   T.fw = d.fw;
   T.iw = d.iw;
   T.cus = d.cus;
-  T.mp_lag = mp_lag();
+  T.prio = ctx->issue_prio;
   return T;
 }
 
@@ -181,21 +162,14 @@ int ensure(nttmul_ctx *ctx, Scratch &sc, void **bufs, int nb, size_t *have, size
   return NTTMUL_OK;
 }
 
-// Polynomials per multi-pass / reordered-transform sub-batch: NTTMUL_MP_CHUNK_MB (default 512) MiB
+// Polynomials per multi-pass / reordered-transform sub-batch: params.scratch_mb (default 512) MiB
 // per scratch buffer (C5: the whole 1024-product batch in one pass).  Smaller sub-batches keep a
 // sub-batch's intermediates in the 256 MiB Infinity Cache but cost more than they save: C5 at
 // 8/16/32/64/128 MiB ran 2.86/1.91/1.60/1.48/1.40 ms against 1.36 ms in one pass
 // (gpurun_out/r2a) — each sub-batch launch is a single generation of blocks.  The
-// bound also caps scratch memory for very large batches.
-size_t env_size(const char *name, size_t dflt) {
-  const char *e = getenv(name);
-  const long v = e ? atol(e) : 0;
-  return v > 0 ? (size_t)v : dflt;
-}
-
-size_t sub_batch(size_t poly_bytes, size_t batch, size_t dflt_mb = 512) {
-  const size_t mb = env_size("NTTMUL_MP_CHUNK_MB", dflt_mb);
-  return std::max<size_t>(1, std::min(batch, (mb << 20) / poly_bytes));
+// bound caps scratch memory for very large batches.
+size_t sub_batch(const nttmul_ctx *ctx, size_t poly_bytes, size_t batch) {
+  return std::max<size_t>(1, std::min(batch, ctx->scratch_bytes / poly_bytes));
 }
 
 int scratch_acquire(nttmul_ctx *ctx, Scratch &sc, hipStream_t s) {
@@ -213,7 +187,7 @@ int scratch_release(nttmul_ctx *ctx, Scratch &sc, hipStream_t s) {
 
 void scratch_free(Scratch &sc) {
   if (sc.used) (void)hipEventSynchronize(sc.ev);
-  for (void *p : {sc.buf[0], sc.buf[1], sc.buf[2], sc.buf[3], sc.perm})
+  for (void *p : {sc.buf[0], sc.buf[1], sc.buf[2], sc.perm})
     if (p) (void)hipFree(p);
   if (sc.ev) (void)hipEventDestroy(sc.ev);
   sc = Scratch();
@@ -228,50 +202,6 @@ enum Op {
   OP_INVERSE = OP_XFORM + (NTTMUL_XF_INVERSE | NTTMUL_XF_REV2STD),
 };
 constexpr unsigned kXfModes = NTTMUL_XF_INVERSE | NTTMUL_XF_REV2STD | NTTMUL_XF_UNSCALED;
-
-// Pipelined multi-pass product (n > 4096, NTTMUL_MP_LANES=2): sub-batches of `chunk` products
-// alternate over the device's lanes (internal streams, each with its own scratch), all ordered
-// after the caller's stream s and joined back into it, so sub-batch i's row pass can overlap
-// sub-batch i + 1's column passes with the lanes' intermediates in the Infinity Cache.  Measured
-// at C5 (profiles/r2/r2_c5_lanes_ab.txt): 1.402-1.427 ms against 1.414-1.425 ms in one pass —
-// the column passes carry a quarter of the butterflies, so the kernels compete for the same VALU
-// and the overlap buys nothing; off by default.
-constexpr size_t kPipeChunkMB = 64;
-int run_lanes(nttmul_ctx *ctx, DevState &d, const LaunchTables &T, const void *a, const void *b,
-              void *c, size_t batch, size_t chunk, int io_bits, hipStream_t s) {
-  const Plan &P = ctx->plan;
-  const size_t io_poly = (size_t)P.n * (io_bits / 8), w_poly = (size_t)P.n * (P.word_bits / 8);
-  if (!d.lanes_in) HIP_TRY(ctx, hipEventCreateWithFlags(&d.lanes_in, hipEventDisableTiming));
-  HIP_TRY(ctx, hipEventRecord(d.lanes_in, s));
-  const int nl = (int)std::min<size_t>(kLanes, (batch + chunk - 1) / chunk);
-  for (int k = 0; k < nl; k++) {
-    Lane &L = d.lane[k];
-    if (!L.s) HIP_TRY(ctx, hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking));
-    HIP_TRY(ctx, hipStreamWaitEvent(L.s, d.lanes_in, 0));
-    int st = scratch_acquire(ctx, L.sc, L.s);
-    if (!st) st = ensure(ctx, L.sc, L.sc.buf, 3, &L.sc.bytes, chunk * w_poly);
-    if (st) return st;
-  }
-  int st = NTTMUL_OK;
-  size_t i = 0;
-  for (size_t p = 0; p < batch && !st; p += chunk, i++) {
-    Lane &L = d.lane[i % nl];
-    const size_t cnt = std::min(chunk, batch - p);
-    hipError_t e = launch_polymul(T, (const char *)a + p * io_poly, (const char *)b + p * io_poly,
-                                  (char *)c + p * io_poly, cnt, io_bits, L.sc.buf, L.s);
-    if (e != hipSuccess) st = fail(ctx, e, "pipelined sub-batch launch");
-  }
-  for (int k = 0; k < nl; k++) {  // join: s continues after every lane's last sub-batch
-    Lane &L = d.lane[k];
-    const int r = scratch_release(ctx, L.sc, L.s);
-    if (!st) st = r;
-    if (!r) {
-      const hipError_t e = hipStreamWaitEvent(s, L.sc.ev, 0);
-      if (e != hipSuccess && !st) st = fail(ctx, e, "hipStreamWaitEvent");
-    }
-  }
-  return st;
-}
 
 void note_product(nttmul_ctx *ctx, const DevState &d, size_t batch, int io_bits, int prio_ok) {
   std::lock_guard<std::mutex> lk(g_err_mu);
@@ -333,22 +263,11 @@ int run_device(nttmul_ctx *ctx, DevState &d, Scratch &sc, int op, void *c, const
     else HIP_TRY(ctx, launch_xform(T, a, c, batch, io_bits, inv, sc.buf, s));
     return NTTMUL_OK;
   }
-  if (multipass && op == OP_MULTIPLY && env_size("NTTMUL_MP_LANES", 1) > 1) {
-    const size_t chunk = sub_batch(w_poly, batch, kPipeChunkMB);
-    if (chunk < batch) {
-      const int st = run_lanes(ctx, d, T, a, b, c, batch, chunk, io_bits, s);
-      if (!st) note_product(ctx, d, chunk, io_bits, T.prio_ok);
-      return st;
-    }
-  }
   // sub-batches through the scratch
-  const size_t chunk = sub_batch(multipass ? w_poly : io_poly, batch);
+  const size_t chunk = sub_batch(ctx, multipass ? w_poly : io_poly, batch);
   int st = scratch_acquire(ctx, sc, s);
   if (st) return st;
   if (multipass && (st = ensure(ctx, sc, sc.buf, 3, &sc.bytes, chunk * w_poly))) return st;
-  if (multipass && op == OP_MULTIPLY && T.mp_lag > 0 &&
-      (st = ensure(ctx, sc, &sc.buf[3], 1, &sc.sync_bytes, mp_sync_bytes(chunk))))
-    return st;
   if (reorder && (st = ensure(ctx, sc, &sc.perm, 1, &sc.perm_bytes, chunk * io_poly))) return st;
   for (size_t p = 0; p < batch && !st; p += chunk) {
     const size_t cnt = std::min(chunk, batch - p);
@@ -365,17 +284,6 @@ int run_device(nttmul_ctx *ctx, DevState &d, Scratch &sc, int op, void *c, const
       e = launch_bitrev(cp, cp, P.logn, cnt, io_bits, s);
     }
     if (e != hipSuccess) st = fail(ctx, e, "sub-batch launch");
-    // NTTMUL_FLAG_VALIDATE: a persistent multi-pass launch whose dependency poll gave up (a
-    // scheduling bug, never a correct run) is reported instead of returning its output
-    if (!st && multipass && op == OP_MULTIPLY && T.mp_lag > 0 && (ctx->flags & NTTMUL_FLAG_VALIDATE)) {
-      unsigned fault = 0;
-      if ((e = hipMemcpyAsync(&fault, (unsigned *)sc.buf[3] + 1, sizeof(fault),
-                              hipMemcpyDeviceToHost, s)) != hipSuccess ||
-          (e = hipStreamSynchronize(s)) != hipSuccess)
-        st = fail(ctx, e, "persistent fault flag");
-      else if (fault)
-        st = fail(ctx, hipErrorLaunchFailure, "k_mp_persist: a dependency wait gave up");
-    }
   }
   if (!st && op == OP_MULTIPLY) note_product(ctx, d, chunk, io_bits, T.prio_ok);
   const int rel = scratch_release(ctx, sc, s);
@@ -385,15 +293,17 @@ int run_device(nttmul_ctx *ctx, DevState &d, Scratch &sc, int op, void *c, const
 // memcpy split over a few host threads for large blocks (the staging copies bound the
 // host-buffer path: one core moves ~10-20 GB/s, a PCIe Gen5 x16 link ~50 GB/s each way).  The
 // workers are started once and live for the process (never joined: the pool is never freed).
+constexpr unsigned kMaxCopyThreads = 64;
 class CopyPool {
  public:
   static CopyPool &get() {
     static CopyPool *pool = new CopyPool();
     return *pool;
   }
-  void copy(void *dst, const void *src, size_t bytes) {
+  // split over at most `threads` threads (the caller's included)
+  void copy(void *dst, const void *src, size_t bytes, unsigned threads) {
     const size_t kPart = 1u << 20;
-    const size_t parts = std::min<size_t>(workers_ + 1, bytes / kPart);
+    const size_t parts = std::min<size_t>(std::min<size_t>(workers_ + 1, threads), bytes / kPart);
     if (parts <= 1) {
       memcpy(dst, src, bytes);
       return;
@@ -418,12 +328,10 @@ class CopyPool {
 
  private:
   CopyPool() {
-    // NTTMUL_COPY_THREADS (default 8, at most the host's hardware threads) staging threads
-    unsigned hw = std::thread::hardware_concurrency();
-    unsigned want = 8;
-    if (const char *e = getenv("NTTMUL_COPY_THREADS")) want = (unsigned)std::max(1, atoi(e));
-    want = std::min(want, std::max(hw, 1u));
-    workers_ = want - 1;
+    // kMaxCopyThreads - 1 workers at most (the host's hardware threads bound it); each call
+    // uses its context's params.copy_threads of them
+    const unsigned hw = std::thread::hardware_concurrency();
+    workers_ = std::min(kMaxCopyThreads, std::max(hw, 1u)) - 1;
     for (unsigned i = 0; i < workers_; i++) std::thread([this, i] { run(i); }).detach();
   }
   void run(unsigned i) {
@@ -452,7 +360,9 @@ class CopyPool {
   const char *s_ = nullptr;
 };
 
-void pcopy(void *dst, const void *src, size_t bytes) { CopyPool::get().copy(dst, src, bytes); }
+void pcopy(const nttmul_ctx *ctx, void *dst, const void *src, size_t bytes) {
+  CopyPool::get().copy(dst, src, bytes, ctx->copy_threads);
+}
 
 int ensure_slots(nttmul_ctx *ctx, DevState &d, size_t bytes) {
   for (int s = 0; s < kSlots; s++)
@@ -527,7 +437,7 @@ int run_host_dev(nttmul_ctx *ctx, DevState &d, const HostJob &J, size_t p0, size
     if (!pd.busy) return NTTMUL_OK;
     pd.busy = false;
     HIP_TRY(ctx, hipStreamSynchronize(d.xs[s]));
-    if (!J.direct) pcopy((char *)J.c + pd.off, d.pin[s][2], pd.bytes);
+    if (!J.direct) pcopy(ctx, (char *)J.c + pd.off, d.pin[s][2], pd.bytes);
     return NTTMUL_OK;
   };
   unsigned k = 0;
@@ -553,8 +463,8 @@ int run_host_dev(nttmul_ctx *ctx, DevState &d, const HostJob &J, size_t p0, size
       continue;
     }
     if ((st = retire(s))) break;
-    pcopy(d.pin[s][0], (const char *)J.a + off, bytes);
-    if (two) pcopy(d.pin[s][1], (const char *)J.b + off, bytes);
+    pcopy(ctx, d.pin[s][0], (const char *)J.a + off, bytes);
+    if (two) pcopy(ctx, d.pin[s][1], (const char *)J.b + off, bytes);
     if (bytes <= J.zero_copy && ctx->plan.logn <= 12) {
       // small transaction (the ntt256_product* shims): the kernel reads a, b from and writes c to
       // the pinned staging buffers over PCIe — no copy-engine round trips
@@ -607,9 +517,8 @@ int run_host(nttmul_ctx *ctx, int op, void *c, const void *a, const void *b, siz
   J.pbytes = (size_t)ctx->plan.n * (io_bits / 8);
   J.chunk = std::max<size_t>(1, kChunkBytes / J.pbytes);
   // per-operand bytes up to which a chunk runs zero-copy on the pinned staging buffers
-  // (NTTMUL_ZEROCOPY_KB, default 64; 0 never)
-  const char *zc_env = getenv("NTTMUL_ZEROCOPY_KB");
-  J.zero_copy = (zc_env ? (size_t)atol(zc_env) : 64) << 10;
+  // (params.zero_copy_kb)
+  J.zero_copy = ctx->zero_copy;
   const size_t total = batch * J.pbytes;
   J.direct = host_pinned(a, total) && (!two || host_pinned(b, total)) && host_pinned(c, total);
   const size_t first_chunk = std::min(J.chunk, std::max<size_t>(1, batch / ctx->ndev));
@@ -686,6 +595,15 @@ int nttmul_create_ex(nttmul_ctx **out, const nttmul_params *prm) {
     return st;
   }
   ctx->flags = prm->flags;
+  if (prm->issue_prio < -1 || prm->issue_prio > 1 || prm->zero_copy_kb < -1 ||
+      prm->copy_threads < 0) {
+    delete ctx;
+    return NTTMUL_EINVAL;
+  }
+  ctx->issue_prio = prm->issue_prio;
+  ctx->zero_copy = prm->zero_copy_kb < 0 ? 0 : (size_t)(prm->zero_copy_kb ? prm->zero_copy_kb : 64) << 10;
+  ctx->copy_threads = prm->copy_threads ? (unsigned)prm->copy_threads : 8u;
+  ctx->scratch_bytes = (size_t)(prm->scratch_mb ? prm->scratch_mb : 512) << 20;
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
     delete ctx;
@@ -752,11 +670,6 @@ void nttmul_destroy(nttmul_ctx *ctx) {
       if (d.xs[k]) (void)hipStreamDestroy(d.xs[k]);
     }
     scratch_free(d.dscr);
-    for (Lane &L : d.lane) {
-      scratch_free(L.sc);
-      if (L.s) (void)hipStreamDestroy(L.s);
-    }
-    if (d.lanes_in) (void)hipEventDestroy(d.lanes_in);
     for (void *p : {d.fw, d.iw, (void *)d.flag})
       if (p) (void)hipFree(p);
     if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -986,5 +899,13 @@ void mulntt256_ct_rev2std(int32_t *a) { transform256(a, 0, kFwdR2S); }
 void mulntt256_ct_std2rev(int32_t *a) { transform256(a, 0, kFwdS2R); }
 void inttmul256_gs_rev2std(int32_t *a) { transform256(a, 0, kInvR2S); }
 void inttmul256_gs_std2rev(int32_t *a) { transform256(a, 0, kInvS2R); }
+
+#ifdef NTTMUL_CLOCK_STAMPS
+// include/nttmul_diag.h (lib/libnttmul_diag.so only)
+int nttmul_diag_clock_stamps(uint64_t *dst, size_t blocks) {
+  if (!dst && blocks) return NTTMUL_EINVAL;
+  return read_clock_stamps(dst, blocks) == hipSuccess ? NTTMUL_OK : NTTMUL_EHIP;
+}
+#endif
 
 }  // extern "C"

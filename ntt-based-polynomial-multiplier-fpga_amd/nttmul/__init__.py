@@ -17,6 +17,8 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_DIR, "lib", "libnttmul.so")
+# the diagnostic build (include/nttmul_diag.h): same kernels plus in-kernel clock stamps
+DIAG_LIB_PATH = os.path.join(PKG_DIR, "lib", "libnttmul_diag.so")
 HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "nttmul.h")
 
 NTTMUL_OK = 0
@@ -58,7 +60,9 @@ class NttmulError(RuntimeError):
 
 class _Params(ctypes.Structure):
     _fields_ = [("n", ctypes.c_uint32), ("q", ctypes.c_uint64), ("psi", ctypes.c_uint64),
-                ("ndev", ctypes.c_int), ("first_dev", ctypes.c_int), ("flags", ctypes.c_uint32)]
+                ("ndev", ctypes.c_int), ("first_dev", ctypes.c_int), ("flags", ctypes.c_uint32),
+                ("issue_prio", ctypes.c_int32), ("zero_copy_kb", ctypes.c_int32),
+                ("copy_threads", ctypes.c_int32), ("scratch_mb", ctypes.c_uint32)]
 
 
 class Info(ctypes.Structure):
@@ -70,6 +74,7 @@ class Info(ctypes.Structure):
 
 
 _LIB: Optional[ctypes.CDLL] = None
+_DIAG_LIB: Optional[ctypes.CDLL] = None
 
 
 def load_library() -> ctypes.CDLL:
@@ -79,7 +84,25 @@ def load_library() -> ctypes.CDLL:
         return _LIB
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} not built: run __graft_entry__.build() or make -C {PKG_DIR}")
-    lib = ctypes.CDLL(LIB_PATH)
+    _LIB = _bind(ctypes.CDLL(LIB_PATH))
+    return _LIB
+
+
+def load_diag_library() -> ctypes.CDLL:
+    """Load lib/libnttmul_diag.so (include/nttmul_diag.h): the same ABI, kernels with in-kernel
+    clock stamps; used by bench.py for the clock the product kernel holds, never for results."""
+    global _DIAG_LIB
+    if _DIAG_LIB is not None:
+        return _DIAG_LIB
+    if not os.path.exists(DIAG_LIB_PATH):
+        raise ImportError(f"{DIAG_LIB_PATH} not built")
+    lib = _bind(ctypes.CDLL(DIAG_LIB_PATH))
+    lib.nttmul_diag_clock_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    _DIAG_LIB = lib
+    return lib
+
+
+def _bind(lib: ctypes.CDLL) -> ctypes.CDLL:
     vp, sz, u64, u32, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
     lib.nttmul_create.argtypes = [ctypes.POINTER(vp), u32, u64, i32]
     lib.nttmul_create_ex.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(_Params)]
@@ -131,7 +154,6 @@ def load_library() -> ctypes.CDLL:
     for name in NTT256_WRAPPERS:
         getattr(lib, name).argtypes = [vp]
         getattr(lib, name).restype = None
-    _LIB = lib
     return lib
 
 
@@ -245,15 +267,20 @@ class Context:
     """An (n, q) multiplier bound to one or more HIP devices (≙ an opened FPGA handle)."""
 
     def __init__(self, n: int, q: int, psi: int = 0, ndev: int = 1, first_dev: int = 0,
-                 validate: bool = False, cyclic: bool = False, share_devices: bool = False):
+                 validate: bool = False, cyclic: bool = False, share_devices: bool = False,
+                 issue_prio: int = 0, zero_copy_kb: int = 0, copy_threads: int = 0,
+                 scratch_mb: int = 0, _lib: Optional[ctypes.CDLL] = None):
         """cyclic=True: FPGA-compat product mod (x^n - 1, q) (Hardware_Multiplier/PolyMult.v);
         `psi` then carries the primitive n-th root omega (0 = the smallest one).
-        share_devices=True: `ndev` slices may map several onto one device (round-robin)."""
-        self._lib = load_library()
+        share_devices=True: `ndev` slices may map several onto one device (round-robin).
+        issue_prio, zero_copy_kb, copy_threads, scratch_mb: the nttmul_params dispatch knobs
+        (include/nttmul.h; 0 = the library default)."""
+        self._lib = load_library() if _lib is None else _lib
         self._h = ctypes.c_void_p()
         flags = ((NTTMUL_FLAG_VALIDATE if validate else 0) | (NTTMUL_FLAG_CYCLIC if cyclic else 0)
                  | (NTTMUL_FLAG_SHARE_DEVICES if share_devices else 0))
-        prm = _Params(n, q, psi, ndev, first_dev, flags)
+        prm = _Params(n, q, psi, ndev, first_dev, flags, issue_prio, zero_copy_kb, copy_threads,
+                      scratch_mb)
         st = self._lib.nttmul_create_ex(ctypes.byref(self._h), ctypes.byref(prm))
         if st != NTTMUL_OK:
             raise NttmulError(st, strerror(st))

@@ -44,6 +44,28 @@ def test_strerror_and_invalid_params():
     assert lib.nttmul_create(ctypes.byref(h), 128, 12289, 1) == nttmul.NTTMUL_EINVAL  # n < 256
 
 
+@pytest.mark.parametrize("field,value", [("issue_prio", 2), ("issue_prio", -2),
+                                         ("zero_copy_kb", -5), ("copy_threads", -1)])
+def test_invalid_dispatch_knobs(field, value):
+    """The nttmul_params dispatch knobs (read once by nttmul_create_ex, include/nttmul.h) are
+    range-checked before any device access: an out-of-range value is NTTMUL_EINVAL."""
+    lib = nttmul.load_library()
+    h = ctypes.c_void_p()
+    p = nttmul._Params(4096, 2013265921, 0, 1, 0, 0)
+    setattr(p, field, value)
+    assert lib.nttmul_create_ex(ctypes.byref(h), ctypes.byref(p)) == nttmul.NTTMUL_EINVAL
+
+
+def test_no_environment_reads_on_the_product_path():
+    """Kernel choice comes from nttmul_params, never from the process environment: the library's
+    sources call getenv nowhere."""
+    src = os.path.join(os.path.dirname(nttmul.LIB_PATH), "..", "csrc")
+    for name in os.listdir(src):
+        if name.endswith((".cpp", ".hip", ".hpp")):
+            text = open(os.path.join(src, name)).read()
+            assert "getenv(" not in text, name
+
+
 @pytest.mark.skipif(os.environ.get("HIP_VISIBLE_DEVICES") is None and os.path.exists("/dev/kfd"),
                     reason="a GPU may be present")
 def test_no_gpu_fails_loudly():

@@ -184,18 +184,11 @@ def test_random_prime_sweep_multipass(n, torch_cuda):
             assert np.array_equal(c[i], P.product_merged(a[i], b[i])), (n, q, i)
 
 
-MP_LAGS = [0, 32]   # NTTMUL_MP_LAG: three launches / the persistent k_mp_persist
-
-
-@pytest.mark.parametrize("lag", MP_LAGS)
 @pytest.mark.parametrize("n", [8192, 16384, 32768, 65536])
 @pytest.mark.parametrize("q", [Q31, Q30, Q32, Q62, Q31HI, Q31LO])
-def test_multipass_vs_oracle(n, q, lag, torch_cuda, monkeypatch):
+def test_multipass_vs_oracle(n, q, torch_cuda):
     """n > 4096: column pass + fused rows + inverse column pass, ragged batch of 3 (and 17 at
-    n = 8192) against the restated reference product (OpenMP batch) and evaluation at roots;
-    as three launches and as one persistent launch (lag 32 > the batch: the whole product is
-    pipeline fill and drain)."""
-    monkeypatch.setenv("NTTMUL_MP_LAG", str(lag))
+    n = 8192) against the restated reference product (OpenMP batch) and evaluation at roots."""
     P = O.Plan(n, q)
     ctx = _ctx(n, q, validate=True)
     assert ctx.info.kernel == 2
@@ -250,27 +243,16 @@ def _check_whole_batch(n, q, word_bits, p0, count, a, b, c, chunk=8192):
     return checked
 
 
-@pytest.mark.parametrize("n,q,word_bits,batch,chunk_mb,lanes,lag", [
-    (4096, Q31, 32, 65536, None, None, None), (1024, Q31, 32, 4096, None, None, None),
-    (65536, Q62, 64, 1024, None, None, 0), (65536, Q62, 64, 1024, None, None, 32),
-    (65536, Q62, 64, 1024, None, None, 4), (65536, Q62, 64, 1024, 64, 2, None),
-    (65536, Q62, 64, 1024, 96, None, 32), (8192, Q31, 32, 2500, 32, None, None),
-    (16384, Q31, 32, 3000, None, None, 32)])
-def test_full_size_device_path(n, q, word_bits, batch, chunk_mb, lanes, lag, torch_cuda,
-                               monkeypatch):
-    """BASELINE configs C3, C2 and C5 at full size on device-resident data, C5 also in 8
-    multi-pass sub-batches over the two pipeline lanes and n = 8192 in three serial sub-batches
-    (NTTMUL_MP_CHUNK_MB / NTTMUL_MP_LANES); C5 both as three launches per product and as one
-    persistent launch (NTTMUL_MP_LAG; lag 4: consumers usually wait for their producers), also
-    in sub-batches: every product against the oracle, bit-exact."""
+@pytest.mark.parametrize("n,q,word_bits,batch,scratch_mb", [
+    (4096, Q31, 32, 65536, 0), (1024, Q31, 32, 4096, 0), (65536, Q62, 64, 1024, 0),
+    (65536, Q62, 64, 1024, 64), (65536, Q62, 64, 1000, 96), (8192, Q31, 32, 2500, 32),
+    (16384, Q31, 32, 3000, 0)])
+def test_full_size_device_path(n, q, word_bits, batch, scratch_mb, torch_cuda):
+    """BASELINE configs C3, C2 and C5 at full size on device-resident data; C5 also in 8 and in
+    6 ragged multi-pass sub-batches and n = 8192 in three (nttmul_params.scratch_mb bounds each
+    scratch buffer): every product against the oracle, bit-exact."""
     torch = torch_cuda
-    if chunk_mb:
-        monkeypatch.setenv("NTTMUL_MP_CHUNK_MB", str(chunk_mb))
-    if lanes:
-        monkeypatch.setenv("NTTMUL_MP_LANES", str(lanes))
-    if lag is not None:
-        monkeypatch.setenv("NTTMUL_MP_LAG", str(lag))
-    ctx = _ctx(n, q, validate=lag is not None)
+    ctx = _ctx(n, q, scratch_mb=scratch_mb)
     dt = _torch_dtype(torch, word_bits)
     a = torch.empty(batch * n, dtype=dt, device="cuda")
     b = torch.empty_like(a)
@@ -311,6 +293,41 @@ def test_issue_priority_variants(n, q, torch_cuda):
     assert not ctx.kernel_name(32).endswith(",prio>")   # batch 0: a large batch
 
 
+@pytest.mark.parametrize("mode", [1, -1])
+def test_issue_priority_forced_by_params(mode, torch_cuda):
+    """nttmul_params.issue_prio = 1 / -1 forces the issue-prioritised / oldest-first fused kernel
+    for every batch size and stream pattern; products stay exact."""
+    torch = torch_cuda
+    n, q, batch = 1024, Q31, 300
+    ctx = _ctx(n, q, issue_prio=mode)
+    want = mode > 0
+    for b in (7, 1 << 20):
+        assert ctx.kernel_name(32, b).endswith(",prio>") == want, (mode, b)
+    a = torch.empty(batch * n, dtype=torch.int32, device="cuda")
+    b_, c = torch.empty_like(a), torch.empty_like(a)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    ctx.fill_random_device(a, b_, 0, batch, 32, stream=s1.cuda_stream)
+    torch.cuda.synchronize()
+    for st in (s1, s2, s1):
+        ctx.multiply_device(c, a, b_, batch, 32, stream=st.cuda_stream)
+        assert ctx.last_kernel_name().endswith(",prio>") == want
+    torch.cuda.synchronize()
+    assert _check_whole_batch(n, q, 32, 0, batch, a, b_, c) == batch
+
+
+@pytest.mark.parametrize("zc,path", [(0, 2), (-1, 0)])
+def test_zero_copy_knob(zc, path, torch_cuda):
+    """nttmul_params.zero_copy_kb: a one-product n = 256 host call runs zero-copy on the pinned
+    staging buffers by default (path 2) and staged through device buffers with -1 (path 0);
+    both give the oracle's product."""
+    n, q = 256, Q31
+    ctx = _ctx(n, q, zero_copy_kb=zc)
+    a, b = O.fill_inputs(n, q, 3, 1)
+    got = ctx.multiply(a.astype(np.uint32), b.astype(np.uint32)).astype(np.uint64)
+    assert ctx.last_host_path() == path
+    assert np.array_equal(got[0], O.Plan(n, q).product_merged(a[0], b[0]))
+
+
 def test_issue_priority_follows_streams(torch_cuda):
     """Calls alternating over two streams overlap, so the library leaves the issue priority off
     for them (nttmul.cpp run_device); consecutive calls on one stream get it.  The last launch is
@@ -338,15 +355,13 @@ def test_issue_priority_follows_streams(torch_cuda):
     assert _check_whole_batch(n, q, 32, 0, batch, a, b, c2) == batch
 
 
-@pytest.mark.parametrize("lag", MP_LAGS)
-def test_c5_bigint_golden(golden_dir, lag, torch_cuda, monkeypatch):
+def test_c5_bigint_golden(golden_dir, torch_cuda):
     """C5 products (n = 65536, q = 0x3FFFFFFFFFE80001) on the device, through the product path the
-    bench runs (device-resident, counter-based inputs at their C5 batch positions) and as one
-    persistent launch: every output word's SHA-256 equals tests/golden/c5_bigint.json, computed by
-    Kronecker substitution with Python big integers -- no NTT, independent of the oracle."""
+    bench runs (device-resident, counter-based inputs at their C5 batch positions): every output
+    word's SHA-256 equals tests/golden/c5_bigint.json, computed by Kronecker substitution with
+    Python big integers -- no NTT, independent of the oracle."""
     import hashlib
     torch = torch_cuda
-    monkeypatch.setenv("NTTMUL_MP_LAG", str(lag))
     g = json.load(open(os.path.join(golden_dir, "c5_bigint.json")))
     n, q = g["n"], g["q"]
     ctx = _ctx(n, q)
@@ -386,17 +401,14 @@ def test_c4_last_rank_slice(torch_cuda):
     assert _check_whole_batch(n, q, 32, p0, count, a, b, c) == count
 
 
-@pytest.mark.parametrize("lanes,lag", [(1, 0), (2, 0), (1, 32)])
-def test_device_calls_on_two_streams(lanes, lag, torch_cuda, monkeypatch):
+@pytest.mark.parametrize("scratch_mb", [0, 32])
+def test_device_calls_on_two_streams(scratch_mb, torch_cuda):
     """Two multi-pass products enqueued back to back on two different streams share the
-    context's scratch (nttmul.cpp Scratch, event-ordered) or, with NTTMUL_MP_LANES=2, its
-    pipeline lanes (run_lanes: each call's two sub-batches run after its own stream and join
-    back into it)."""
+    context's scratch (nttmul.cpp Scratch, event-ordered), also when each call runs in
+    sub-batches through it (scratch_mb 32: three per call)."""
     torch = torch_cuda
-    monkeypatch.setenv("NTTMUL_MP_LANES", str(lanes))
-    monkeypatch.setenv("NTTMUL_MP_LAG", str(lag))
     n, q, batch = 16384, Q31, 1200
-    ctx = _ctx(n, q)
+    ctx = _ctx(n, q, scratch_mb=scratch_mb)
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
     a = torch.empty(batch * n, dtype=torch.int32, device="cuda")
     b = torch.empty_like(a)
@@ -704,11 +716,14 @@ def test_transform_modes_device(torch_cuda):
         assert torch.equal(back, a)
 
 
-def test_bench_two_ranks_on_one_gpu(tmp_path, torch_cuda):
+@pytest.mark.parametrize("world,batch", [(2, 4096), (8, 1024)])
+def test_bench_ranks_on_one_gpu(world, batch, tmp_path, torch_cuda):
     """bench.py's N > 1 path as the driver launches it (torch.distributed.run, one process per
-    rank, gloo control plane), with both ranks on this box's GPU(s): the JSON line reports the
-    global batch, and the products each rank dumps from its own slice equal the oracle's at their
-    global counter positions (rank 1 owns [batch, 2 batch))."""
+    rank, gloo control plane: barrier + all_reduce(MAX)), with every rank on this box's GPU(s):
+    2 ranks, and the 8-rank SCALE run's control plane (--gpus 8, 1024 products per rank).  The
+    JSON line reports n_gpus and the global batch, and the products each rank dumps from its own
+    contiguous slice [k batch, (k + 1) batch) equal the oracle's at their global
+    counter positions."""
     import socket
     import subprocess
     import sys
@@ -716,22 +731,24 @@ def test_bench_two_ranks_on_one_gpu(tmp_path, torch_cuda):
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
         port = so.getsockname()[1]
-    batch = 4096
     prefix = str(tmp_path / "samples")
     out = subprocess.run(
-        [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-         "--master-addr", "127.0.0.1", "--master-port", str(port),
-         os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
-         "--no-cpu-baseline", "--batch-per-gpu", str(batch), "--dump-samples", prefix],
+        [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
+         str(world), "--master-addr", "127.0.0.1", "--master-port", str(port),
+         os.path.join(root, "bench.py"), "--gpus", str(world), "--steps", "3", "--warmup", "1",
+         "--settle-ms", "20", "--no-cpu-baseline", "--batch-per-gpu", str(batch),
+         "--dump-samples", prefix],
         capture_output=True, text=True, timeout=300, cwd=root)
     assert out.returncode == 0, out.stderr[-3000:]
     line = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
-    assert line["n_gpus"] == 2 and line["config"]["global_batch"] == 2 * batch
+    assert line["n_gpus"] == world and line["config"]["global_batch"] == world * batch
     assert line["config"]["batch_per_gpu"] == batch and line["value"] > 0
+    assert line["scaling"] == "weak"
     P = O.Plan(4096, Q31)
-    for r in range(2):
+    for r in range(world):
         d = np.load(f"{prefix}.rank{r}.npz")
         assert int(d["p0"]) == r * batch and int(d["p1"]) == (r + 1) * batch
+        assert int(d["world"]) == world and int(d["global_batch"]) == world * batch
         for i, row in zip(d["idx"], d["c"]):
             ea, eb = O.fill_inputs(4096, Q31, int(d["p0"]) + int(i), 1)
             assert np.array_equal(row, P.product_merged(ea[0], eb[0])), (r, int(i))

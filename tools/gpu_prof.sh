@@ -22,8 +22,8 @@ one() {  # cfg name, bench args...
   run 300 python bench.py "$@" > $OUT/bench.json 2> $OUT/bench.err
   tail -c 700 $OUT/bench.json >&2
   run 300 rocprofv3 --kernel-trace --stats -T -d $OUT/trace -o trace --output-format csv -- \
-    python3 bench.py --no-cpu-baseline --power-seconds 0 "$@" > $OUT/trace.log 2>&1
-  run 900 tools/profile_pmc.sh $OUT/pmc "$@" --no-cpu-baseline --power-seconds 0 --settle-ms 0 --steps 3 --warmup 1 > $OUT/pmc.log 2>&1
+    python3 bench.py --no-cpu-baseline --power-seconds 0 --clock-seconds 0 "$@" > $OUT/trace.log 2>&1
+  run 900 tools/profile_pmc.sh $OUT/pmc "$@" --no-cpu-baseline --power-seconds 0 --clock-seconds 0 --settle-ms 0 --steps 3 --warmup 1 > $OUT/pmc.log 2>&1
 }
 for cfg in $CFGS; do
   case $cfg in
