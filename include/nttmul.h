@@ -74,6 +74,12 @@ typedef struct {
                            host's hardware threads                                              */
   uint32_t scratch_mb;  /* n > 4096 products and reordered transforms: at most this many MiB per
                            scratch buffer; larger batches run in sub-batches through it [512]   */
+  int32_t small_server; /* host-buffer products of at most 1024 words per operand (n <= 1024,
+                           q < 2^31, 32-bit words): 0 = served by a resident one-wave device
+                           kernel that polls a page-locked mailbox, the FPGA's GO / done-all
+                           handshake without a launch per call [automatic; the kernel leaves
+                           after 20 ms without a request and is relaunched on demand];
+                           -1 = a kernel launch per call                                        */
 } nttmul_params;
 
 typedef struct {
@@ -110,7 +116,8 @@ int nttmul_kernel_name_batch(const nttmul_ctx *ctx, int word_bits, size_t batch,
 int nttmul_last_kernel_name(const nttmul_ctx *ctx, char *buf, size_t cap);
 /* Diagnostics: how the last host-buffer call on ctx moved its first chunk: 0 staged through
  * pinned buffers, 1 direct DMA from / to page-locked caller memory, 2 zero-copy kernel access to
- * the pinned staging buffers; -1 before any call. */
+ * the pinned staging buffers, 3 the resident device server's mailbox (params.small_server);
+ * -1 before any call. */
 int nttmul_last_host_path(const nttmul_ctx *ctx);
 
 /* multiply(a, b, n, q) -> c for one polynomial; host buffers of n words.

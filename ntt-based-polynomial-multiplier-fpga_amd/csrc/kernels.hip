@@ -898,6 +898,72 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
   CLK_STAMP(1);
 }
 
+// Small-transaction device server (host calls of at most 1024 words per operand, e.g. the
+// reference's ntt256_product4 through the compat shims; nttmul.cpp Server).  One resident wave
+// polls the mailbox's go word in host memory (system-scope loads, s_sleep between polls); on a
+// new sequence number it takes the request (system acquire), loads a and b from the mailbox,
+// runs the same fused product as k_rows (64 / (n / 16) products per wave, exchanges ordered per
+// wave), stores c, releases (system) and publishes done = seq.  It leaves on stop, after
+// idle_ticks without a request or after life_ticks in all (the host relaunches it on demand), so
+// the wave always ends -- the FPGA's GO / done-all handshake without a kernel launch per call.
+template <class A, int LOGS>
+__global__ __launch_bounds__(64) void k_server(KParams<A> P, ServerBox *box,
+                                               unsigned long long idle_ticks,
+                                               unsigned long long life_ticks) {
+  using W = typename A::word;
+  using Gr = Groups<LOGS, kWT<A, LOGS>()>;
+  constexpr int N = Gr::N, TP = N / 16, PB = 64 / TP, G = Gr::G, NP = Gr::NP;
+  static_assert(sizeof(W) == 4 && TP <= 64, "u32 words, n <= 1024");
+  __shared__ W lds[PB][NP];
+  const int pb = threadIdx.x / TP, j = threadIdx.x % TP;
+  W *lx = lds[pb];
+  constexpr int D = NTTMUL_BASE_D ? A::kBaseD : 0;
+  unsigned seen = __hip_atomic_load(&box->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  seen = __builtin_amdgcn_readfirstlane(seen);
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long last = t0;
+  for (;;) {
+    const unsigned go = __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(&box->go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    const unsigned stop = __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(&box->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+    if (stop) break;
+    if (go == seen) {
+      if (now - last > idle_ticks || now - t0 > life_ticks) break;
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the host's a, b, count before go
+    const int count = (int)__builtin_amdgcn_readfirstlane(box->count);
+    const bool live = pb < count;
+    const int base = (live ? pb : 0) * N + Gr::base(0, j);
+    W x[16], y[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      x[k] = box->a[base + Gr::off(0, k)];
+      y[k] = box->b[base + Gr::off(0, k)];
+    }
+    TwPair<W> zw[16];
+    fwd_all<A, LOGS, 0, 2, D, 1>(P.ar, x, y, lx, lx, P.fw, j, 0, 0, zw);
+    base_mult<A, LOGS, D>(P.ar, x, y, zw, j);
+    inv_all<A, LOGS, G - 1, true, D, 1>(P, x, y, lx, lx, P.iw, j, 0, 0);
+    if (live) {
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        W v = x[k];
+        if (!A::kInvCanonical) v = P.ar.canon(v);
+        box->c[base + Gr::off(0, k)] = v;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // c reaches host memory before done
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(&box->done, go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    seen = go;
+    last = now;
+  }
+}
+
 // C2 in-launch overlap experiments (tools/kbench builds only: both measured slower
 // than k_rows at C2 and at n = 1024 x 262144, profiles/r3/c2/)
 #ifdef NTTMUL_KBENCH_BUILD
@@ -1772,6 +1838,19 @@ static hipError_t launch_polymul_(const LaunchTables &T, const void *a, const vo
   }
   return polymul_io<Arith64>(T, a, b, c, batch, io_bits, scr, s);
 #endif
+}
+
+hipError_t launch_server(const LaunchTables &T, ServerBox *box, unsigned long long idle_ticks,
+                         unsigned long long life_ticks, hipStream_t s) {
+  if (T.word_bits != 32 || a32_kind(T.q) != A32Kind::Plantard || T.logn < 8 || T.logn > 10)
+    return hipErrorNotSupported;
+  const KParams<Arith32P> P = product_params<Arith32P>(T);
+  switch (T.logn) {
+    case 8: hipLaunchKernelGGL((k_server<Arith32P, 8>), dim3(1), dim3(64), 0, s, P, box, idle_ticks, life_ticks); break;
+    case 9: hipLaunchKernelGGL((k_server<Arith32P, 9>), dim3(1), dim3(64), 0, s, P, box, idle_ticks, life_ticks); break;
+    default: hipLaunchKernelGGL((k_server<Arith32P, 10>), dim3(1), dim3(64), 0, s, P, box, idle_ticks, life_ticks); break;
+  }
+  return hipGetLastError();
 }
 
 hipError_t describe_polymul(const LaunchTables &T, int io_bits, size_t batch, std::string *out) {

@@ -20,6 +20,7 @@
 #include <condition_variable>
 #include <mutex>
 #include <string>
+#include <chrono>
 #include <thread>
 #include <vector>
 
@@ -74,6 +75,21 @@ struct DevState {
   std::atomic<uintptr_t> prod_s{0};  // (uintptr_t)stream | 1 (the null stream is a stream too); 0: none
 };
 
+// The small-transaction device server (kernels.hip k_server): its mailbox in page-locked,
+// host-coherent memory and the stream its resident kernel runs on.
+struct Server {
+  ServerBox *box = nullptr;
+  ServerBox *dbox = nullptr;                  // the mailbox as a device pointer
+  hipStream_t s = nullptr;
+  unsigned seq = 0;                           // last request posted
+  bool running = false;                       // launched and not known to have left
+  std::chrono::steady_clock::time_point launched, last_done;
+};
+constexpr unsigned long long kServerIdleTicks = 2000000;  // 20 ms at 100 MHz (s_memrealtime)
+constexpr unsigned long long kServerLifeTicks = 100000000; // 1 s
+constexpr auto kServerIdleHost = std::chrono::milliseconds(10);   // host-side margins: past
+constexpr auto kServerLifeHost = std::chrono::milliseconds(500);  // these, stop and relaunch
+
 }  // namespace
 
 struct nttmul_ctx {
@@ -87,6 +103,8 @@ struct nttmul_ctx {
   size_t zero_copy = 64u << 10;               // per-operand bytes run zero-copy (0: never)
   unsigned copy_threads = 8;
   size_t scratch_bytes = (size_t)512 << 20;   // per scratch buffer
+  int small_server = 0;                       // 0 automatic, -1 never
+  Server server;                              // on dev[0]
   int last_path = -1;                         // run_host: 0 staged, 1 direct DMA, 2 zero-copy
   // the last product launch (run_device, under g_err_mu): nttmul_last_kernel_name re-describes it
   struct {
@@ -496,6 +514,93 @@ int run_host_dev(nttmul_ctx *ctx, DevState &d, const HostJob &J, size_t p0, size
   return st;
 }
 
+// Small host transactions (params.small_server; kernels.hip k_server): the FPGA flow's mode 3 +
+// WaitForDoneAll (NTT_PCIECommunicationv2.c:83-107, 211-215) without a kernel launch per call.
+// The caller's a, b go into the mailbox, go = seq releases them, and the host spins on done;
+// the resident kernel is (re)launched when it is not known to be alive: never launched, idle on
+// the host's clock for longer than kServerIdleHost (it leaves after 20 ms on its own), older than
+// kServerLifeHost, or found finished while a request waits.  Every spin is bounded.
+int server_stop(nttmul_ctx *ctx) {
+  Server &S = ctx->server;
+  if (!S.running) return NTTMUL_OK;
+  __atomic_store_n(&S.box->stop, 1u, __ATOMIC_RELEASE);
+  S.running = false;
+  const hipError_t e = hipStreamSynchronize(S.s);
+  __atomic_store_n(&S.box->stop, 0u, __ATOMIC_RELEASE);
+  return e == hipSuccess ? NTTMUL_OK : fail(ctx, e, "device server exit");
+}
+
+int server_launch(nttmul_ctx *ctx, DevState &d) {
+  Server &S = ctx->server;
+  HIP_TRY(ctx, launch_server(tables_for(ctx, d), S.dbox, kServerIdleTicks, kServerLifeTicks, S.s));
+  S.running = true;
+  S.launched = S.last_done = std::chrono::steady_clock::now();
+  return NTTMUL_OK;
+}
+
+// >0: not served here (the caller takes the launch path); else a status
+int run_server(nttmul_ctx *ctx, void *c, const void *a, const void *b, size_t batch) {
+  const Plan &P = ctx->plan;
+  const size_t words = batch * P.n;
+  if (ctx->small_server < 0 || ctx->ndev != 1 || P.word_bits != 32 || P.logn < 8 || P.logn > 10 ||
+      words > (size_t)ServerBox::kWords || a32_kind(P.q) != A32Kind::Plantard)
+    return 1;
+  if (ctx->flags & NTTMUL_FLAG_VALIDATE) {  // the range check of run_device, on the host
+    const uint32_t *pa = (const uint32_t *)a, *pb = (const uint32_t *)b;
+    for (size_t i = 0; i < words; i++)
+      if (pa[i] >= P.q || pb[i] >= P.q) {
+        snprintf(ctx->err, sizeof(ctx->err), "input coefficient >= q");
+        return NTTMUL_ERANGE;
+      }
+  }
+  Server &S = ctx->server;
+  DevState &d = ctx->dev[0];
+  HIP_TRY(ctx, hipSetDevice(d.id));
+  if (!S.box) {
+    HIP_TRY(ctx, hipHostMalloc((void **)&S.box, sizeof(ServerBox), hipHostMallocCoherent));
+    memset((void *)S.box, 0, sizeof(ServerBox));
+    HIP_TRY(ctx, hipHostGetDevicePointer((void **)&S.dbox, S.box, 0));
+    HIP_TRY(ctx, hipStreamCreateWithFlags(&S.s, hipStreamNonBlocking));
+  }
+  const auto now = std::chrono::steady_clock::now();
+  if (S.running && (now - S.last_done > kServerIdleHost || now - S.launched > kServerLifeHost)) {
+    const int st = server_stop(ctx);
+    if (st) return st;
+  }
+  if (!S.running) {
+    const int st = server_launch(ctx, d);
+    if (st) return st;
+  }
+  memcpy(S.box->a, a, words * 4);
+  memcpy(S.box->b, b, words * 4);
+  S.box->count = (uint32_t)batch;
+  const unsigned seq = ++S.seq;
+  __atomic_store_n(&S.box->go, seq, __ATOMIC_RELEASE);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned spin = 1; __atomic_load_n(&S.box->done, __ATOMIC_ACQUIRE) != seq; spin++) {
+    __builtin_ia32_pause();
+    if (spin % 4096) continue;
+    const hipError_t q = hipStreamQuery(S.s);
+    if (q == hipSuccess) {           // the kernel left before it saw this request: relaunch
+      S.running = false;
+      const int st = server_launch(ctx, d);
+      if (st) return st;
+    } else if (q != hipErrorNotReady) {
+      S.running = false;
+      return fail(ctx, q, "device server");
+    }
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+      (void)server_stop(ctx);
+      snprintf(ctx->err, sizeof(ctx->err), "device server: no answer within 5 s");
+      return NTTMUL_EHIP;
+    }
+  }
+  memcpy(c, S.box->c, words * 4);
+  S.last_done = std::chrono::steady_clock::now();
+  ctx->last_path = 3;
+  return NTTMUL_OK;
+}
+
 // The batch splits into one contiguous slice per context device; with several devices each slice
 // is driven by its own host thread (slice 0 by the caller's), so one device's staging copies and
 // synchronisations never stall another's pipeline.
@@ -508,6 +613,10 @@ int run_host(nttmul_ctx *ctx, int op, void *c, const void *a, const void *b, siz
   if (io_bits == 32 && ctx->plan.q > 0xFFFFFFFFull) return NTTMUL_EINVAL;
   if (!batch) return NTTMUL_OK;
   DeviceGuard guard;
+  if (op == OP_MULTIPLY && io_bits == 32) {
+    const int st = run_server(ctx, c, a, b, batch);
+    if (st <= 0) return st;
+  }
   HostJob J;
   J.op = op;
   J.io_bits = io_bits;
@@ -604,6 +713,11 @@ int nttmul_create_ex(nttmul_ctx **out, const nttmul_params *prm) {
   ctx->zero_copy = prm->zero_copy_kb < 0 ? 0 : (size_t)(prm->zero_copy_kb ? prm->zero_copy_kb : 64) << 10;
   ctx->copy_threads = prm->copy_threads ? (unsigned)prm->copy_threads : 8u;
   ctx->scratch_bytes = (size_t)(prm->scratch_mb ? prm->scratch_mb : 512) << 20;
+  if (prm->small_server < -1 || prm->small_server > 0) {
+    delete ctx;
+    return NTTMUL_EINVAL;
+  }
+  ctx->small_server = prm->small_server;
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
     delete ctx;
@@ -655,6 +769,12 @@ int nttmul_create(nttmul_ctx **ctx, uint32_t n, uint64_t q, int ndev) {
 void nttmul_destroy(nttmul_ctx *ctx) {
   if (!ctx) return;
   DeviceGuard guard;
+  if (ctx->server.box) {
+    (void)hipSetDevice(ctx->dev[0].id);
+    (void)server_stop(ctx);
+    if (ctx->server.s) (void)hipStreamDestroy(ctx->server.s);
+    (void)hipHostFree(ctx->server.box);
+  }
   for (int i = 0; i < ctx->ndev; i++) {
     DevState &d = ctx->dev[i];
     if (d.id < 0) continue;

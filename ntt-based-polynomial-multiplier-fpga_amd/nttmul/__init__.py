@@ -62,7 +62,8 @@ class _Params(ctypes.Structure):
     _fields_ = [("n", ctypes.c_uint32), ("q", ctypes.c_uint64), ("psi", ctypes.c_uint64),
                 ("ndev", ctypes.c_int), ("first_dev", ctypes.c_int), ("flags", ctypes.c_uint32),
                 ("issue_prio", ctypes.c_int32), ("zero_copy_kb", ctypes.c_int32),
-                ("copy_threads", ctypes.c_int32), ("scratch_mb", ctypes.c_uint32)]
+                ("copy_threads", ctypes.c_int32), ("scratch_mb", ctypes.c_uint32),
+                ("small_server", ctypes.c_int32)]
 
 
 class Info(ctypes.Structure):
@@ -269,18 +270,19 @@ class Context:
     def __init__(self, n: int, q: int, psi: int = 0, ndev: int = 1, first_dev: int = 0,
                  validate: bool = False, cyclic: bool = False, share_devices: bool = False,
                  issue_prio: int = 0, zero_copy_kb: int = 0, copy_threads: int = 0,
-                 scratch_mb: int = 0, _lib: Optional[ctypes.CDLL] = None):
+                 scratch_mb: int = 0, small_server: int = 0,
+                 _lib: Optional[ctypes.CDLL] = None):
         """cyclic=True: FPGA-compat product mod (x^n - 1, q) (Hardware_Multiplier/PolyMult.v);
         `psi` then carries the primitive n-th root omega (0 = the smallest one).
         share_devices=True: `ndev` slices may map several onto one device (round-robin).
-        issue_prio, zero_copy_kb, copy_threads, scratch_mb: the nttmul_params dispatch knobs
-        (include/nttmul.h; 0 = the library default)."""
+        issue_prio, zero_copy_kb, copy_threads, scratch_mb, small_server: the nttmul_params
+        dispatch knobs (include/nttmul.h; 0 = the library default)."""
         self._lib = load_library() if _lib is None else _lib
         self._h = ctypes.c_void_p()
         flags = ((NTTMUL_FLAG_VALIDATE if validate else 0) | (NTTMUL_FLAG_CYCLIC if cyclic else 0)
                  | (NTTMUL_FLAG_SHARE_DEVICES if share_devices else 0))
         prm = _Params(n, q, psi, ndev, first_dev, flags, issue_prio, zero_copy_kb, copy_threads,
-                      scratch_mb)
+                      scratch_mb, small_server)
         st = self._lib.nttmul_create_ex(ctypes.byref(self._h), ctypes.byref(prm))
         if st != NTTMUL_OK:
             raise NttmulError(st, strerror(st))
@@ -313,7 +315,8 @@ class Context:
             raise NttmulError(st, f"{strerror(st)}: {self._lib.nttmul_last_error(self._h).decode()}")
 
     def last_host_path(self) -> int:
-        """nttmul_last_host_path: 0 staged, 1 direct DMA, 2 zero-copy, -1 no call yet."""
+        """nttmul_last_host_path: 0 staged, 1 direct DMA, 2 zero-copy, 3 device server, -1 no
+        call yet."""
         return int(self._lib.nttmul_last_host_path(self._h))
 
     def kernel_name(self, word_bits: int = 0, batch: int = 0) -> str:

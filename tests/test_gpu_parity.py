@@ -319,9 +319,10 @@ def test_issue_priority_forced_by_params(mode, torch_cuda):
 def test_zero_copy_knob(zc, path, torch_cuda):
     """nttmul_params.zero_copy_kb: a one-product n = 256 host call runs zero-copy on the pinned
     staging buffers by default (path 2) and staged through device buffers with -1 (path 0);
-    both give the oracle's product."""
+    both give the oracle's product.  (small_server = -1: such a call otherwise goes to the
+    resident device server, path 3.)"""
     n, q = 256, Q31
-    ctx = _ctx(n, q, zero_copy_kb=zc)
+    ctx = _ctx(n, q, zero_copy_kb=zc, small_server=-1)
     a, b = O.fill_inputs(n, q, 3, 1)
     got = ctx.multiply(a.astype(np.uint32), b.astype(np.uint32)).astype(np.uint64)
     assert ctx.last_host_path() == path
@@ -603,6 +604,64 @@ def test_time_testing_gpu_app(golden_dir, torch_cuda):
     vals = [int(x) for line in out.split("Resultado C = A * B):")[1].split("\n") for x in line.split()]
     assert vals == [int(v) for v in g["ntt256_product4"][0]]
     assert "Batch 1024" in out
+
+
+@pytest.mark.parametrize("n,batch", [(256, 1), (256, 4), (256, 3), (512, 2), (1024, 1)])
+def test_small_server_products(n, batch, torch_cuda):
+    """Host calls of at most 1024 words per operand run on the resident device server
+    (nttmul.cpp run_server, kernels.hip k_server: the mailbox in page-locked memory, GO / done
+    sequence words): last_host_path 3, products equal the oracle's, over many back-to-back
+    calls with changing inputs (every request a new sequence number); small_server = -1 takes
+    the launch-per-call path (2) with the same results."""
+    q = Q31
+    P = O.Plan(n, q)
+    srv, launch = _ctx(n, q), _ctx(n, q, small_server=-1)
+    for it in range(40):
+        a, b = O.fill_inputs(n, q, 100 * it, batch)
+        a, b = a.astype(np.uint32), b.astype(np.uint32)
+        if it == 7:
+            a[0] = q - 1
+        got = srv.multiply(a, b).astype(np.uint64)
+        assert srv.last_host_path() == 3
+        for i in range(batch):
+            assert np.array_equal(got[i], P.product_merged(a[i], b[i])), (it, i)
+        if it % 10 == 0:
+            assert np.array_equal(launch.multiply(a, b).astype(np.uint64), got)
+            assert launch.last_host_path() == 2
+
+
+def test_small_server_restarts(torch_cuda):
+    """The server kernel leaves after 20 ms without a request and at most 1 s after its launch;
+    the host stops and relaunches it past its own 10 ms / 0.5 s margins.  Calls across idle gaps
+    and past the lifetime stay exact; a context destroyed while its server runs stops it; the
+    reference-width validation (NTTMUL_FLAG_VALIDATE) is done on the host for this path."""
+    import time
+    n, q = 256, 12289
+    P = O.Plan(n, q, 1002)
+    ctx = _ctx(n, q, psi=1002, validate=True)
+    t0 = time.time()
+    k = 0
+    for gap in (0, 0.005, 0.015, 0.03, 0.0, 0.06):
+        time.sleep(gap)
+        a, b = O.fill_inputs(n, q, k, 1)
+        k += 1
+        got = ctx.multiply(a.astype(np.uint32), b.astype(np.uint32)).astype(np.uint64)
+        assert ctx.last_host_path() == 3
+        assert np.array_equal(got[0], P.product_merged(a[0], b[0]))
+    while time.time() - t0 < 1.2:     # past the host's 0.5 s and the kernel's 1 s lifetime
+        a, b = O.fill_inputs(n, q, k, 1)
+        k += 1
+        got = ctx.multiply(a.astype(np.uint32), b.astype(np.uint32)).astype(np.uint64)
+        assert np.array_equal(got[0], P.product_merged(a[0], b[0])), k
+    bad = a.astype(np.uint32)
+    bad[0, 5] = q
+    with pytest.raises(nttmul.NttmulError) as ei:
+        ctx.multiply(bad, b.astype(np.uint32))
+    assert ei.value.status == nttmul.NTTMUL_ERANGE
+    ctx.close()                       # stops the running server kernel
+    ctx2 = _ctx(n, q, psi=1002)
+    got = ctx2.multiply(a.astype(np.uint32), b.astype(np.uint32)).astype(np.uint64)
+    assert np.array_equal(got[0], P.product_merged(a[0], b[0]))
 
 
 @pytest.mark.parametrize("n,q,batch", [(4096, Q31, 1537), (256, Q30, 20000), (1024, Q62, 1100),
