@@ -110,7 +110,8 @@
 // libnttmul.so
 #if (NTTMUL_ABL_TWMASK || NTTMUL_ABL_NOLOAD || NTTMUL_ABL_NOXCHG || NTTMUL_ABL_NOSTORE || \
      NTTMUL_ABL_BOUNDQ || NTTMUL_ABL_PERMXCHG || \
-     NTTMUL_KBENCH_LITE || defined(NTTMUL_ABL_L2LOAD) || defined(NTTMUL_STAGGER)) && \
+     NTTMUL_KBENCH_LITE || defined(NTTMUL_ABL_L2LOAD) || defined(NTTMUL_STAGGER) || \
+     defined(NTTMUL_ABL_L2CI) || defined(NTTMUL_ABL_L2CF)) && \
     !defined(NTTMUL_KBENCH_BUILD)
 #error "NTTMUL_ABL_* / NTTMUL_KBENCH_LITE are wrong-result kbench switches (tools/kbench/build.sh only)"
 #endif
@@ -788,8 +789,9 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
   // threads past the batch end read unit 0 (always valid) instead of branching per load; their
   // results are never stored
   const size_t base_l = live ? base_g : (size_t)Gr::base(0, j);
-#ifdef NTTMUL_ABL_L2LOAD  // ablation: every unit reads one of the first 64 units (L2-resident)
-  const size_t base_r = (u & 63) * N + Gr::base(0, j);
+#ifdef NTTMUL_ABL_L2LOAD  // ablation: every unit reads one of the first NTTMUL_ABL_L2LOAD units
+                          // (default 64; L2-resident)
+  const size_t base_r = (u % (NTTMUL_ABL_L2LOAD > 1 ? NTTMUL_ABL_L2LOAD : 64)) * N + Gr::base(0, j);
 #else
   const size_t base_r = base_l;
 #endif
@@ -935,7 +937,8 @@ __global__ __launch_bounds__(64) void k_server(KParams<A> P, ServerBox *box,
       continue;
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the host's a, b, count before go
-    const int count = (int)__builtin_amdgcn_readfirstlane(box->count);
+    const int count = (int)__builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(&box->count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
     const bool live = pb < count;
     const int base = (live ? pb : 0) * N + Gr::base(0, j);
     W x[16], y[16];
@@ -1213,11 +1216,16 @@ __global__ __launch_bounds__(256) void k_cols_fwd(KParams<A> P, const TIn *__res
   if (gid >= batch * ncol) return;
   const size_t p = gid >> logs, col = gid & (ncol - 1);
   const size_t base = (p << (logs + L1)) + col;
+#ifdef NTTMUL_ABL_L2CF  // kbench ablation: every polynomial reads polynomial 0 (L2-resident)
+  const size_t base_r = col;
+#else
+  const size_t base_r = base;
+#endif
   W x[M], y[M];
 #pragma clang loop unroll(full)
   for (int m = 0; m < M; m++) {
-    x[m] = (W)ld_stream<NTTMUL_NT_COLS>(a + base + ((size_t)m << logs));
-    y[m] = NPOLY == 2 ? (W)ld_stream<NTTMUL_NT_COLS>(b + base + ((size_t)m << logs)) : W(0);
+    x[m] = (W)ld_stream<NTTMUL_NT_COLS>(a + base_r + ((size_t)m << logs));
+    y[m] = NPOLY == 2 ? (W)ld_stream<NTTMUL_NT_COLS>(b + base_r + ((size_t)m << logs)) : W(0);
   }
 #pragma clang loop unroll(full)
   for (int st = 0; st < L1; st++) {
@@ -1249,9 +1257,14 @@ __global__ __launch_bounds__(256) void k_cols_inv(KParams<A> P,
   if (gid >= batch * ncol) return;
   const size_t p = gid >> logs, col = gid & (ncol - 1);
   const size_t base = (p << (logs + L1)) + col;
+#ifdef NTTMUL_ABL_L2CI  // kbench ablation: every polynomial reads polynomial 0's rows (L2-resident)
+  const size_t base_r = col;
+#else
+  const size_t base_r = base;
+#endif
   W x[M];
 #pragma clang loop unroll(full)
-  for (int m = 0; m < M; m++) x[m] = ld_stream<NTTMUL_NT_COLS>(tc + base + ((size_t)m << logs));
+  for (int m = 0; m < M; m++) x[m] = ld_stream<NTTMUL_NT_COLS>(tc + base_r + ((size_t)m << logs));
 #pragma clang loop unroll(full)
   for (int st = L1 - 1; st >= 0; st--) {
     const int dist = M >> (st + 1);

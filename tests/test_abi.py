@@ -85,7 +85,8 @@ def test_no_device_host_alloc():
 
 @pytest.mark.parametrize("flag", ["NTTMUL_ABL_NOLOAD", "NTTMUL_ABL_NOXCHG", "NTTMUL_ABL_NOSTORE",
                                   "NTTMUL_ABL_TWMASK", "NTTMUL_KBENCH_LITE", "NTTMUL_ABL_L2LOAD",
-                                  "NTTMUL_ABL_BOUNDQ", "NTTMUL_ABL_PERMXCHG", "NTTMUL_STAGGER"])
+                                  "NTTMUL_ABL_BOUNDQ", "NTTMUL_ABL_PERMXCHG", "NTTMUL_STAGGER",
+                                  "NTTMUL_ABL_L2CI", "NTTMUL_ABL_L2CF"])
 def test_ablation_switches_refuse_library_build(flag):
     """The wrong-result kbench ablation switches cannot reach libnttmul.so: kernels.hip stops with
     #error unless NTTMUL_KBENCH_BUILD is also defined (tools/kbench/build.sh only)."""

@@ -16,3 +16,5 @@ timeout -k 10 300 python bench.py > $OUT/c3_bench.json 2> $OUT/c3_bench.err || {
 tail -c 1800 $OUT/c3_bench.json
 timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/driver_cmd.json 2> $OUT/driver_cmd.err || { tail -20 $OUT/driver_cmd.err; exit 1; }
 tail -c 300 $OUT/driver_cmd.json
+bash tools/r4/c5_l2_ablation.sh ${1:-r4b}_c5l2 > /dev/null || exit 1
+cat gpurun_out/${1:-r4b}_c5l2/ab.txt
