@@ -1565,6 +1565,7 @@ static KParams<A> make_params(const LaunchTables &T) {
   KParams<A> P;
   P.ar.q = (W)T.q;
   P.ar.qinv_neg = (W)T.qinv_neg;
+  if constexpr (std::is_same<A, Arith64>::value) P.ar.q2 = 2 * T.q;
   if constexpr (IsPlantard<A>::value) {
     P.ar.c32 = (uint32_t)((1ull << 32) % T.q);
     P.ar.as = (uint32_t)((3 * T.q + 1) / 2);
@@ -1614,6 +1615,9 @@ static bool rows_prio(size_t waves) {
   return waves <= (size_t)tl_prio_cus * 4 * 4;  // 4 SIMDs per CU, 4 waves per SIMD
 }
 
+#ifdef NTTMUL_KBENCH_BUILD
+static thread_local int tl_rows_lds_extra = 0;  // LaunchTables::rows_lds_extra of the current call
+#endif
 template <class A, class TIn, class TOut, int LOGS, int L1>
 static hipError_t launch_rows(const KParams<A> &P, const void *a, const void *b, void *c,
                               size_t units, hipStream_t s) {
@@ -1636,7 +1640,12 @@ static hipError_t launch_rows(const KParams<A> &P, const void *a, const void *b,
       return hipGetLastError();
     }
   }
-  hipLaunchKernelGGL((k_rows<A, TIn, TOut, LOGS, L1>), dim3((unsigned)blocks), dim3(NT), 0, s, P,
+#ifdef NTTMUL_KBENCH_BUILD
+  const unsigned dyn = L1 > 0 ? (unsigned)tl_rows_lds_extra : 0u;
+#else
+  constexpr unsigned dyn = 0;
+#endif
+  hipLaunchKernelGGL((k_rows<A, TIn, TOut, LOGS, L1>), dim3((unsigned)blocks), dim3(NT), dyn, s, P,
                      (const TIn *)a, (const TIn *)b, (TOut *)c, units);
   return hipGetLastError();
 }
@@ -1718,15 +1727,30 @@ static hipError_t multipass_l1(const LaunchTables &T, const void *a, const void 
     describe_add("k_cols_inv<" + args + ">");
     return hipSuccess;
   }
-  hipLaunchKernelGGL((k_cols_fwd<A, IO, L1>), dim3(cblocks), dim3(256), 0, s, P, (const IO *)a,
-                     (const IO *)b, (W *)ta, (W *)tb, batch, LOGS);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  e = launch_rows<A, W, W, LOGS, L1>(P, ta, tb, tc, batch << L1, s);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((k_cols_inv<A, IO, L1>), dim3(cblocks), dim3(256), 0, s, P,
-                     (const W *)tc, (IO *)c, batch, LOGS);
-  return hipGetLastError();
+#ifdef NTTMUL_KBENCH_BUILD
+  // (kbench: one pass only, T.mp_phase >= 0; the row pass with T.rows_lds_extra bytes of LDS)
+  const int phase = T.mp_phase;
+  tl_rows_lds_extra = T.rows_lds_extra;
+#else
+  constexpr int phase = -1;
+#endif
+  hipError_t e = hipSuccess;
+  if (phase < 0 || phase == 0) {
+    hipLaunchKernelGGL((k_cols_fwd<A, IO, L1>), dim3(cblocks), dim3(256), 0, s, P, (const IO *)a,
+                       (const IO *)b, (W *)ta, (W *)tb, batch, LOGS);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  if (phase < 0 || phase == 1) {
+    e = launch_rows<A, W, W, LOGS, L1>(P, ta, tb, tc, batch << L1, s);
+    if (e != hipSuccess) return e;
+  }
+  if (phase < 0 || phase == 2) {
+    hipLaunchKernelGGL((k_cols_inv<A, IO, L1>), dim3(cblocks), dim3(256), 0, s, P,
+                       (const W *)tc, (IO *)c, batch, LOGS);
+    e = hipGetLastError();
+  }
+  return e;
 }
 
 #ifdef NTTMUL_KBENCH_BUILD

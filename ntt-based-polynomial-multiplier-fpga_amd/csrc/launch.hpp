@@ -28,6 +28,10 @@ struct LaunchTables {
   int mp_lag = 0;            // n > 4096: > 0 = one persistent launch (k_mp_persist) with this
                              // many steps between a polynomial's column, row and inverse tasks
   void *mp_stats = nullptr;  // NTTMUL_MP_STATS builds: 9 u64 task statistics
+  int mp_phase = -1;         // n > 4096: -1 all three passes, 0 only k_cols_fwd, 1 only the row
+                             // pass, 2 only k_cols_inv (sub-batch pipelines across streams)
+  int rows_lds_extra = 0;    // n > 4096: dynamic LDS bytes added to each row-pass workgroup (caps
+                             // the row pass's workgroups per CU, leaving room for column waves)
   int pipe_per_wave = 0;     // tools/kbench builds, n = 1024, q < 2^31, u32: > 0 = k_rows_pipe with this many products
                              // per wave (loads of the next one issued before the current one's
                              // transforms); 0 = one product per one-wave workgroup (k_rows)

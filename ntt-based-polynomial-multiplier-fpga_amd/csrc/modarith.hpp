@@ -591,6 +591,10 @@ struct Arith32W {
 #ifndef NTTMUL_A64_MADC
 #define NTTMUL_A64_MADC 1
 #endif
+// CT sum output through the Shoup product's addend (Arith64::ct; tools/kbench A/B)
+#ifndef NTTMUL_A64_ACC
+#define NTTMUL_A64_ACC 1
+#endif
 struct Arith64 {
   using word = uint64_t;
   static constexpr int kBits = 64;
@@ -598,6 +602,8 @@ struct Arith64 {
   static constexpr bool kInvCanonical = false;
   uint64_t q;
   uint64_t qinv_neg;  // -q^-1 mod 2^64
+  uint64_t q2;        // 2q, set by the host: opaque to the compiler, so 2x + q2 stays one
+                      // v_lshl_add_u64 (from 2q it folds 2x + 2q into 2 (x + q), two instructions)
 
   // x in [0, 2m) -> [0, m).  Spelled as a 32-bit borrow chain so the select uses the borrow of
   // v_subb_co_u32 directly (the 64-bit __builtin_sub_overflow form adds a v_cmp_gt_u64).
@@ -668,23 +674,27 @@ struct Arith64 {
     return ((uint64_t)hi << 32) | (uint32_t)a;
 #endif
   }
-  // x * w mod q in [0, 2q) for any 64-bit x (Shoup, w' = floor(w 2^64 / q))
+  // acc + (x * w mod q, in [0, 2q)) mod 2^64 for any 64-bit x (Shoup, w' = floor(w 2^64 / q)).
+  // The addend rides in the 64-bit addend of the first v_mad_u64_u32 (a constant 0 otherwise), so
+  // a Harvey CT gets its sum output x + t without an add of its own (NTTMUL_A64_ACC).
   template <bool MADC = true>
-  __device__ __forceinline__ uint64_t shoup(uint64_t x, uint64_t w, uint64_t ws) const {
+  __device__ __forceinline__ uint64_t shoup(uint64_t x, uint64_t w, uint64_t ws,
+                                            uint64_t acc = 0) const {
     const uint64_t qh = mulhi64<MADC>(x, ws);
 #if NTTMUL_A64_V2
     // lo64(x w) - lo64(qh q) in one pass: D = xl wl + hl (2^32 - ql) carries the low word and a
     // high word off by +hl, which the complemented constants absorb (2 v_mad_u64_u32,
-    // 4 v_mul_lo_u32, 2 v_add3_u32; no 64-bit subtract chain)
+    // 4 v_mul_lo_u32, 2 v_add3_u32; no 64-bit subtract chain).  Everything is mod 2^64, so acc
+    // can join the low sum.
     const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
     const uint32_t wl = (uint32_t)w, wh = (uint32_t)(w >> 32);
     const uint32_t hl = (uint32_t)qh, hh = (uint32_t)(qh >> 32);
     const uint32_t nql = 0u - (uint32_t)q, nqh1 = ~(uint32_t)(q >> 32);
-    const uint64_t D = (uint64_t)xl * wl + (uint64_t)hl * nql;
+    const uint64_t D = (uint64_t)xl * wl + acc + (uint64_t)hl * nql;
     const uint32_t hi = (uint32_t)(D >> 32) + xl * wh + xh * wl + hl * nqh1 + hh * nql;
     return ((uint64_t)hi << 32) | (uint32_t)D;
 #else
-    return mullo64(x, w) - mullo64(qh, q);
+    return acc + mullo64(x, w) - mullo64(qh, q);
 #endif
   }
 #if NTTMUL_A64_PLAIN
@@ -710,13 +720,21 @@ struct Arith64 {
   __device__ __forceinline__ uint64_t canon(uint64_t x) const { return csub(x, q); }
 #else
   static constexpr uint64_t kLazy = 4;  // forward values in [0, 4q), inverse values in [0, 2q)
-  // Harvey CT: X in [0, 4q), any Y -> outputs in [0, 4q)
+  // Harvey CT: X in [0, 4q), any Y -> outputs in [0, 4q).  NTTMUL_A64_ACC: the sum comes out of
+  // the Shoup product's addend and the difference is 2x + 2q - (x + t) (one v_lshl_add_u64 and a
+  // 64-bit subtract), one VALU instruction less than x + t and (x + 2q) - t.
   template <bool XC = false>
   __device__ __forceinline__ void ct(uint64_t &X, uint64_t &Y, uint64_t w, uint64_t ws) const {
     const uint64_t x = XC ? X : csub(X, 2 * q);
+#if NTTMUL_A64_ACC
+    const uint64_t s = shoup(Y, w, ws, x);
+    X = s;
+    Y = (x << 1) + q2 - s;
+#else
     const uint64_t t = shoup(Y, w, ws);
     X = x + t;
     Y = x - t + 2 * q;
+#endif
   }
   // Harvey GS: X, Y in [0, 2q) -> outputs in [0, 2q)
   __device__ __forceinline__ void gs(uint64_t &X, uint64_t &Y, uint64_t w, uint64_t ws) const {

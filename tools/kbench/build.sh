@@ -1,11 +1,11 @@
 #!/bin/bash
 # Build kbench variants: tools/kbench/build.sh [VARIANT=-Dflags ...]
-# (KB_FLAGS defaults to -DNTTMUL_KBENCH_LITE=1: only the n <= 4096, q < 2^31 product kernels;
+# (KB_OUT: output directory, default tools/kbench/bin; KB_FLAGS defaults to -DNTTMUL_KBENCH_LITE=1: only the n <= 4096, q < 2^31 product kernels;
 #  KB_FLAGS=" " builds every kernel)
 set -e
 R=$(cd "$(dirname "$0")/../.." && pwd)
 P=$R/ntt-based-polynomial-multiplier-fpga_amd
-OUT=$R/tools/kbench/bin
+OUT=${KB_OUT:-$R/tools/kbench/bin}
 mkdir -p $OUT
 build() {
   local name=$1; shift

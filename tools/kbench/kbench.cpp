@@ -72,7 +72,63 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&ra[i], bytes)); CK(hipMalloc(&rb[i], bytes)); CK(hipMalloc(&rc[i], bytes));
     CK(nttmul::launch_fill(ra[i], rb[i], P.logn, q, 0x4E54544D554Cull, 0, batch, io_bits, 0));
   }
-  for (int i = 0; i < 3; i++) CK(nttmul::launch_polymul(T, a, b, c, batch, io_bits, scr, 0));
+  // KB_ROWS_LDS=B: the row pass of an n > 4096 product takes B more bytes of LDS per workgroup
+  // (caps its workgroups per CU, so column-pass waves can be resident beside it)
+  T.rows_lds_extra = getenv("KB_ROWS_LDS") ? atoi(getenv("KB_ROWS_LDS")) : 0;
+  // KB_SUB=S (n > 4096): the batch runs as sub-batches of S products through a ring of three
+  // scratch sets, the row passes on one stream and the column passes on another, issued so that
+  // the columns of sub-batch i + 1 and the inverse columns of i - 1 can overlap the rows of i
+  const size_t sub = getenv("KB_SUB") ? strtoull(getenv("KB_SUB"), 0, 0) : 0;
+  if (sub) {
+    if (P.logn <= 12 || batch % sub) { fprintf(stderr, "KB_SUB needs n > 4096 and sub | batch\n"); return 1; }
+    for (int i = 0; i < 3; i++) CK(hipFree(scr[i]));
+  }
+  void *ring[3][3];
+  hipStream_t scol = 0, srow = 0;
+  constexpr int kEv = 16;
+  hipEvent_t evcf[kEv], evr[kEv];
+  size_t gsub = 0;  // sub-batches issued so far (ring position)
+  if (sub) {
+    for (int r = 0; r < 3; r++)
+      for (int i = 0; i < 3; i++) CK(hipMalloc(&ring[r][i], sub * n * (P.word_bits / 8)));
+    CK(hipStreamCreateWithFlags(&scol, hipStreamNonBlocking));
+    CK(hipStreamCreateWithFlags(&srow, hipStreamNonBlocking));
+    for (int i = 0; i < kEv; i++) {
+      CK(hipEventCreateWithFlags(&evcf[i], hipEventDisableTiming));
+      CK(hipEventCreateWithFlags(&evr[i], hipEventDisableTiming));
+    }
+  }
+  auto pipelined = [&](void *pa, void *pb, void *pc) {
+    const size_t ns = batch / sub, step = sub * n * wb;
+    auto pass = [&](int phase, size_t g, size_t i, hipStream_t s) {
+      nttmul::LaunchTables t = T;
+      t.mp_phase = phase;
+      CK(nttmul::launch_polymul(t, (char *)pa + i * step, (char *)pb + i * step,
+                                (char *)pc + i * step, sub, io_bits, ring[g % 3], s));
+    };
+    pass(0, gsub, 0, scol);
+    CK(hipEventRecord(evcf[gsub % kEv], scol));
+    for (size_t i = 0; i < ns; i++) {
+      const size_t g = gsub + i;
+      CK(hipStreamWaitEvent(srow, evcf[g % kEv], 0));
+      pass(1, g, i, srow);
+      CK(hipEventRecord(evr[g % kEv], srow));
+      if (i + 1 < ns) {
+        pass(0, g + 1, i + 1, scol);
+        CK(hipEventRecord(evcf[(g + 1) % kEv], scol));
+      }
+      CK(hipStreamWaitEvent(scol, evr[g % kEv], 0));
+      pass(2, g, i, scol);
+    }
+    gsub += ns;
+  };
+  if (sub) {
+    CK(hipDeviceSynchronize());  // the fills ran on the null stream
+    for (int i = 0; i < 3; i++) pipelined(a, b, c);
+    CK(hipDeviceSynchronize());
+  } else {
+    for (int i = 0; i < 3; i++) CK(nttmul::launch_polymul(T, a, b, c, batch, io_bits, scr, 0));
+  }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   // KB_STREAMS=2: consecutive launches alternate over two streams with their own c buffer (a and
@@ -88,10 +144,19 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&c2, bytes));
     CK(hipDeviceSynchronize());
   }
-  CK(hipEventRecord(e0, st[0]));
+  if (!sub) CK(hipEventRecord(e0, st[0]));
   if (nstreams == 2) {
     CK(hipEventRecord(join, st[0]));
     CK(hipStreamWaitEvent(st[1], join, 0));
+  }
+  if (sub) {  // the column stream times the run; the row stream joins it at both ends
+    CK(hipEventRecord(e0, scol));
+    CK(hipStreamWaitEvent(srow, e0, 0));
+    for (int i = 0; i < reps; i++) pipelined(a, b, c);
+    CK(hipEventRecord(join, srow));
+    CK(hipStreamWaitEvent(scol, join, 0));
+    st[0] = scol;
+    reps = -reps;  // (skip the loop below)
   }
   for (int i = 0; i < reps; i++) {
     const int k = nstreams == 2 ? (i & 1) : 0;
@@ -110,6 +175,7 @@ int main(int argc, char **argv) {
   CK(hipEventSynchronize(e1));
   float ms;
   CK(hipEventElapsedTime(&ms, e0, e1));
+  if (reps < 0) reps = -reps;
   ms /= reps;
   double pps = batch / (ms * 1e-3);
   double gbs = 3.0 * n * wb * batch / (ms * 1e-3) / 1e9;

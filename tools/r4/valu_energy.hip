@@ -5,6 +5,7 @@
 // it samples board power, and divides power by the lane-op rate.  Block 0..blocks-1 also stamp
 // s_memtime / s_memrealtime around their loop (a buffer of their own; no output depends on
 // them), so the clock each kind runs at is read in-kernel.
+// Build: hipcc --offload-arch=gfx950 -O3 -shared -fPIC valu_energy.hip -o libvalu_energy.so
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -67,6 +68,18 @@ __global__ __launch_bounds__(256) void ve(uint32_t *out, unsigned long long *sta
       if constexpr (KIND == 11) OP1("v_mul_hi_u32_u24");
       if constexpr (KIND == 12) asm volatile("v_fma_f32 %0, %0, %1, %1" : "+v"(f[i]) : "v"(fk));
       if constexpr (KIND == 13) asm volatile("v_lshl_add_u32 %0, %0, 3, %1" : "+v"(v[i]) : "v"(k));
+      // (kinds 2 and 11 chain v = mulhi(v, k), which shrinks v towards 0 within a few steps, so
+      // their operands stop toggling and their energy reads low; kinds 14-16 keep the operands
+      // random with v ^= op(v, k): energy(op) = 2 x pair - energy(v_xor_b32))
+      if constexpr (KIND == 14 || KIND == 15 || KIND == 16) {
+        uint32_t tmp;
+        if constexpr (KIND == 14)
+          asm volatile("v_mul_hi_u32 %1, %0, %2\n\tv_xor_b32 %0, %0, %1" : "+v"(v[i]), "=&v"(tmp) : "v"(k));
+        if constexpr (KIND == 15)
+          asm volatile("v_mul_hi_u32_u24 %1, %0, %2\n\tv_xor_b32 %0, %0, %1" : "+v"(v[i]), "=&v"(tmp) : "v"(k));
+        if constexpr (KIND == 16)
+          asm volatile("v_mul_lo_u32 %1, %0, %2\n\tv_xor_b32 %0, %0, %1" : "+v"(v[i]), "=&v"(tmp) : "v"(k));
+      }
     }
   }
   if (threadIdx.x == 0) {
@@ -82,16 +95,19 @@ __global__ __launch_bounds__(256) void ve(uint32_t *out, unsigned long long *sta
 }
 
 extern "C" {
-int ve_kinds() { return 14; }
+int ve_kinds() { return 17; }
 const char *ve_name(int kind) {
   static const char *n[] = {"v_add_u32", "v_mul_lo_u32", "v_mul_hi_u32", "v_mad_u64_u32",
                             "v_mul_u32_u24", "v_mad_u32_u24", "v_fma_f64", "v_mul_f64",
                             "v_sub_co_u32+v_cndmask_b32 (pair)", "v_xor_b32", "s_sleep (no VALU)",
-                            "v_mul_hi_u32_u24", "v_fma_f32", "v_lshl_add_u32"};
-  return kind >= 0 && kind < 14 ? n[kind] : "";
+                            "v_mul_hi_u32_u24", "v_fma_f32", "v_lshl_add_u32",
+                            "v_mul_hi_u32+v_xor_b32 (pair, random operands)",
+                            "v_mul_hi_u32_u24+v_xor_b32 (pair, random operands)",
+                            "v_mul_lo_u32+v_xor_b32 (pair, random operands)"};
+  return kind >= 0 && kind < 17 ? n[kind] : "";
 }
 // VALU instructions per lane per loop iteration
-int ve_ops_per_iter(int kind) { return kind == 8 ? 2 * CH : kind == 10 ? 0 : CH; }
+int ve_ops_per_iter(int kind) { return kind == 8 || kind >= 14 ? 2 * CH : kind == 10 ? 0 : CH; }
 int ve_launch(int kind, void *out, void *stamps, int blocks, int iters, void *stream) {
   hipStream_t s = (hipStream_t)stream;
   uint32_t *o = (uint32_t *)out;
@@ -99,6 +115,7 @@ int ve_launch(int kind, void *out, void *stamps, int blocks, int iters, void *st
 #define L(K) case K: hipLaunchKernelGGL(ve<K>, dim3(blocks), dim3(256), 0, s, o, st, 12345u + K, iters); break
   switch (kind) {
     L(0); L(1); L(2); L(3); L(4); L(5); L(6); L(7); L(8); L(9); L(10); L(11); L(12); L(13);
+    L(14); L(15); L(16);
     default: return -1;
   }
 #undef L
