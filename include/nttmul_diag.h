@@ -23,6 +23,14 @@ extern "C" {
  * has completed. */
 int nttmul_diag_clock_stamps(uint64_t *dst, size_t blocks);
 
+/* The resident device server's timeline of ctx's last host product served through it
+ * (nttmul_last_host_path == 3; params.small_server): dst[0..3] = s_memrealtime (100 MHz) when
+ * the kernel saw the request, had a and b loaded, had the product computed, had c stored and
+ * released; dst[4], dst[5] = s_memtime (shader clock) around the product; dst[6] = host
+ * nanoseconds from posting the request to seeing it done.  NTTMUL_EINVAL if the last call did not
+ * go through the server. */
+int nttmul_diag_server_stamps(const nttmul_ctx *ctx, uint64_t *dst);
+
 #ifdef __cplusplus
 }
 #endif

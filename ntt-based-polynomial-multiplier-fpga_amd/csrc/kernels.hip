@@ -937,6 +937,10 @@ __global__ __launch_bounds__(64) void k_server(KParams<A> P, ServerBox *box,
       continue;
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the host's a, b, count before go
+#ifdef NTTMUL_CLOCK_STAMPS
+    unsigned long long st[6];
+    st[0] = __builtin_amdgcn_s_memrealtime();
+#endif
     const int count = (int)__builtin_amdgcn_readfirstlane(
         __hip_atomic_load(&box->count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
     const bool live = pb < count;
@@ -948,9 +952,19 @@ __global__ __launch_bounds__(64) void k_server(KParams<A> P, ServerBox *box,
       y[k] = box->b[base + Gr::off(0, k)];
     }
     TwPair<W> zw[16];
+#ifdef NTTMUL_CLOCK_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    st[1] = __builtin_amdgcn_s_memrealtime();
+    st[4] = __builtin_amdgcn_s_memtime();
+#endif
     fwd_all<A, LOGS, 0, 2, D, 1>(P.ar, x, y, lx, lx, P.fw, j, 0, 0, zw);
     base_mult<A, LOGS, D>(P.ar, x, y, zw, j);
     inv_all<A, LOGS, G - 1, true, D, 1>(P, x, y, lx, lx, P.iw, j, 0, 0);
+#ifdef NTTMUL_CLOCK_STAMPS
+    __builtin_amdgcn_sched_barrier(0);
+    st[2] = __builtin_amdgcn_s_memrealtime();
+    st[5] = __builtin_amdgcn_s_memtime();
+#endif
     if (live) {
 #pragma unroll
       for (int k = 0; k < 16; k++) {
@@ -961,6 +975,13 @@ __global__ __launch_bounds__(64) void k_server(KParams<A> P, ServerBox *box,
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // c reaches host memory before done
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef NTTMUL_CLOCK_STAMPS
+    st[3] = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0)  // vector stores from lane 0, released with done below
+      for (int k = 0; k < 6; k++) box->stamp[k] = st[k];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
     __hip_atomic_store(&box->done, go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     seen = go;
     last = now;
@@ -1216,8 +1237,9 @@ __global__ __launch_bounds__(256) void k_cols_fwd(KParams<A> P, const TIn *__res
   if (gid >= batch * ncol) return;
   const size_t p = gid >> logs, col = gid & (ncol - 1);
   const size_t base = (p << (logs + L1)) + col;
-#ifdef NTTMUL_ABL_L2CF  // kbench ablation: every polynomial reads polynomial 0 (L2-resident)
-  const size_t base_r = col;
+#ifdef NTTMUL_ABL_L2CF  // kbench ablation: polynomial p reads polynomial p mod NTTMUL_ABL_L2CF
+                        // (1: one polynomial, L2-resident; 32: 64 MiB, Infinity-Cache-resident)
+  const size_t base_r = ((p % (NTTMUL_ABL_L2CF > 1 ? NTTMUL_ABL_L2CF : 1)) << (logs + L1)) + col;
 #else
   const size_t base_r = base;
 #endif
@@ -1257,8 +1279,9 @@ __global__ __launch_bounds__(256) void k_cols_inv(KParams<A> P,
   if (gid >= batch * ncol) return;
   const size_t p = gid >> logs, col = gid & (ncol - 1);
   const size_t base = (p << (logs + L1)) + col;
-#ifdef NTTMUL_ABL_L2CI  // kbench ablation: every polynomial reads polynomial 0's rows (L2-resident)
-  const size_t base_r = col;
+#ifdef NTTMUL_ABL_L2CI  // kbench ablation: polynomial p reads polynomial p mod NTTMUL_ABL_L2CI's
+                        // rows (1: L2-resident; 32: Infinity-Cache-resident)
+  const size_t base_r = ((p % (NTTMUL_ABL_L2CI > 1 ? NTTMUL_ABL_L2CI : 1)) << (logs + L1)) + col;
 #else
   const size_t base_r = base;
 #endif

@@ -75,6 +75,9 @@ struct ServerBox {
   alignas(128) uint32_t a[kWords];
   alignas(128) uint32_t b[kWords];
   alignas(128) uint32_t c[kWords];
+  // lib/libnttmul_diag.so: the last request's s_memrealtime stamps (request seen, a and b
+  // loaded, product computed, c stored and released) and s_memtime around the product
+  alignas(128) unsigned long long stamp[6];
 };
 // Launch the server for products of n = 2^logn <= 1024 u32 words (q < 2^31) on stream s; it
 // leaves after idle_ticks of the 100 MHz clock without a request, after life_ticks in all, or

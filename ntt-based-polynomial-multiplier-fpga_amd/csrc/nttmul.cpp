@@ -82,6 +82,7 @@ struct Server {
   ServerBox *dbox = nullptr;                  // the mailbox as a device pointer
   hipStream_t s = nullptr;
   unsigned seq = 0;                           // last request posted
+  uint64_t host_ns = 0;                       // go -> done seen on the host, last request
   bool running = false;                       // launched and not known to have left
   std::chrono::steady_clock::time_point launched, last_done;
 };
@@ -575,8 +576,8 @@ int run_server(nttmul_ctx *ctx, void *c, const void *a, const void *b, size_t ba
   memcpy(S.box->b, b, words * 4);
   S.box->count = (uint32_t)batch;
   const unsigned seq = ++S.seq;
-  __atomic_store_n(&S.box->go, seq, __ATOMIC_RELEASE);
   const auto t0 = std::chrono::steady_clock::now();
+  __atomic_store_n(&S.box->go, seq, __ATOMIC_RELEASE);
   for (unsigned spin = 1; __atomic_load_n(&S.box->done, __ATOMIC_ACQUIRE) != seq; spin++) {
     __builtin_ia32_pause();
     if (spin % 4096) continue;
@@ -595,8 +596,9 @@ int run_server(nttmul_ctx *ctx, void *c, const void *a, const void *b, size_t ba
       return NTTMUL_EHIP;
     }
   }
-  memcpy(c, S.box->c, words * 4);
   S.last_done = std::chrono::steady_clock::now();
+  S.host_ns = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(S.last_done - t0).count();
+  memcpy(c, S.box->c, words * 4);
   ctx->last_path = 3;
   return NTTMUL_OK;
 }
@@ -1025,6 +1027,13 @@ void inttmul256_gs_std2rev(int32_t *a) { transform256(a, 0, kInvS2R); }
 int nttmul_diag_clock_stamps(uint64_t *dst, size_t blocks) {
   if (!dst && blocks) return NTTMUL_EINVAL;
   return read_clock_stamps(dst, blocks) == hipSuccess ? NTTMUL_OK : NTTMUL_EHIP;
+}
+int nttmul_diag_server_stamps(const nttmul_ctx *ctx, uint64_t *dst) {
+  if (!ctx || !dst) return NTTMUL_EINVAL;
+  if (!ctx->server.box || ctx->last_path != 3) return NTTMUL_EINVAL;
+  for (int k = 0; k < 6; k++) dst[k] = __atomic_load_n(&ctx->server.box->stamp[k], __ATOMIC_ACQUIRE);
+  dst[6] = ctx->server.host_ns;
+  return NTTMUL_OK;
 }
 #endif
 
