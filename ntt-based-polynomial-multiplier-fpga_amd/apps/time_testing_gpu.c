@@ -56,6 +56,7 @@ int main(int argc, char **argv) {
     sum += now() - t0;
   }
   printf("Tempo total medio ntt256 gs (GPU): %.3f ms\n", sum / num_inter * 1000);
+  printf("(%.2f us por chamada, %d chamadas)\n", sum / num_inter * 1e6, num_inter);
 
   if (batch > 1) {
     nttmul_ctx *ctx = NULL;

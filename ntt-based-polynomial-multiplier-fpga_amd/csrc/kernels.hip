@@ -902,12 +902,17 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
 
 // Small-transaction device server (host calls of at most 1024 words per operand, e.g. the
 // reference's ntt256_product4 through the compat shims; nttmul.cpp Server).  One resident wave
-// polls the mailbox's go word in host memory (system-scope loads, s_sleep between polls); on a
-// new sequence number it takes the request (system acquire), loads a and b from the mailbox,
-// runs the same fused product as k_rows (64 / (n / 16) products per wave, exchanges ordered per
-// wave), stores c, releases (system) and publishes done = seq.  It leaves on stop, after
-// idle_ticks without a request or after life_ticks in all (the host relaunches it on demand), so
-// the wave always ends -- the FPGA's GO / done-all handshake without a kernel launch per call.
+// polls the mailbox's go word (sequence number << 8 | product count) in host memory with two
+// system-scope reads in flight; on a new word it takes the request (system acquire), pulls a and
+// b from the mailbox in
+// 16-byte loads into LDS (every load a PCIe read: the whole request in as few, wide reads as
+// possible), runs the same fused product as k_rows (64 / (n / 16) products per wave, exchanges
+// ordered per wave), stages c in LDS and writes it back in 16-byte stores, releases (system) and
+// publishes done = the go word.  A single product of n <= 512 transforms a and b on two lane groups at
+// once (each group one polynomial, b's result handed to a's lanes by lane permutes) instead of
+// both on one group.  It leaves on stop, after idle_ticks without a request or after life_ticks
+// in all (the host relaunches it on demand), so the wave always ends -- the FPGA's GO / done-all
+// handshake without a kernel launch per call.
 template <class A, int LOGS>
 __global__ __launch_bounds__(64) void k_server(KParams<A> P, ServerBox *box,
                                                unsigned long long idle_ticks,
@@ -916,48 +921,76 @@ __global__ __launch_bounds__(64) void k_server(KParams<A> P, ServerBox *box,
   using Gr = Groups<LOGS, kWT<A, LOGS>()>;
   constexpr int N = Gr::N, TP = N / 16, PB = 64 / TP, G = Gr::G, NP = Gr::NP;
   static_assert(sizeof(W) == 4 && TP <= 64, "u32 words, n <= 1024");
+  constexpr int KW = ServerBox::kWords;
   __shared__ W lds[PB][NP];
-  const int pb = threadIdx.x / TP, j = threadIdx.x % TP;
+  __shared__ uint4 stg[2][KW / 4];  // a, b as loaded (c as stored reuses stg[0])
+  const int lane = threadIdx.x, pb = lane / TP, j = lane % TP;
   W *lx = lds[pb];
   constexpr int D = NTTMUL_BASE_D ? A::kBaseD : 0;
   unsigned seen = __hip_atomic_load(&box->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   seen = __builtin_amdgcn_readfirstlane(seen);
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   unsigned long long last = t0;
+  // two polls in flight: the next read of go is issued before the previous one is waited for,
+  // so a request is seen about half a PCIe round trip sooner than by one poll at a time
+  unsigned pend = __hip_atomic_load(&box->go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   for (;;) {
-    const unsigned go = __builtin_amdgcn_readfirstlane(
-        __hip_atomic_load(&box->go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-    const unsigned stop = __builtin_amdgcn_readfirstlane(
-        __hip_atomic_load(&box->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    __builtin_amdgcn_s_sleep(1);
+    const unsigned next = __hip_atomic_load(&box->go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned go = __builtin_amdgcn_readfirstlane(pend);
+    pend = next;
     const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-    if (stop) break;
     if (go == seen) {
       if (now - last > idle_ticks || now - t0 > life_ticks) break;
-      __builtin_amdgcn_s_sleep(1);
       continue;
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the host's a, b, count before go
+    const int count = (int)(go & 0xFFu);
+    if (count == (int)ServerBox::kStop || count > PB) {  // stop (count > PB: never posted)
+      __hip_atomic_store(&box->done, go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the host's a, b before go
 #ifdef NTTMUL_CLOCK_STAMPS
     unsigned long long st[6];
     st[0] = __builtin_amdgcn_s_memrealtime();
 #endif
-    const int count = (int)__builtin_amdgcn_readfirstlane(
-        __hip_atomic_load(&box->count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    const int q4 = count * (N / 4);  // 16-byte quads per operand (count <= PB, so <= KW / 4)
+    {
+      const uint4 *ga = (const uint4 *)box->a, *gb = (const uint4 *)box->b;
+      for (int i = lane; i < q4; i += 64) {
+        stg[0][i] = ga[i];
+        stg[1][i] = gb[i];
+      }
+    }
+    xsync<1>();
+    const W *sa = (const W *)stg[0], *sb = (const W *)stg[1];
+    // one product of n <= 512: lane group 0 transforms a, group 1 b (then hands b over)
+    const bool split = PB >= 2 && count == 1;
     const bool live = pb < count;
-    const int base = (live ? pb : 0) * N + Gr::base(0, j);
     W x[16], y[16];
+    {
+      const int base = (live ? pb : 0) * N + Gr::base(0, j);
+      const W *src = split && pb == 1 ? sb : sa;
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-      x[k] = box->a[base + Gr::off(0, k)];
-      y[k] = box->b[base + Gr::off(0, k)];
+      for (int k = 0; k < 16; k++) {
+        x[k] = src[base + Gr::off(0, k)];
+        y[k] = sb[base + Gr::off(0, k)];
+      }
     }
     TwPair<W> zw[16];
 #ifdef NTTMUL_CLOCK_STAMPS
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     st[1] = __builtin_amdgcn_s_memrealtime();
     st[4] = __builtin_amdgcn_s_memtime();
 #endif
-    fwd_all<A, LOGS, 0, 2, D, 1>(P.ar, x, y, lx, lx, P.fw, j, 0, 0, zw);
+    if (split) {
+      fwd_all<A, LOGS, 0, 1, D, 1>(P.ar, x, y, lx, lx, P.fw, j, 0, 0, zw);
+#pragma unroll
+      for (int k = 0; k < 16; k++)  // group 1's transformed b to group 0's lanes, same j
+        y[k] = (W)__builtin_amdgcn_ds_bpermute((lane + TP) << 2, (int)x[k]);
+    } else {
+      fwd_all<A, LOGS, 0, 2, D, 1>(P.ar, x, y, lx, lx, P.fw, j, 0, 0, zw);
+    }
     base_mult<A, LOGS, D>(P.ar, x, y, zw, j);
     inv_all<A, LOGS, G - 1, true, D, 1>(P, x, y, lx, lx, P.iw, j, 0, 0);
 #ifdef NTTMUL_CLOCK_STAMPS
@@ -965,13 +998,20 @@ __global__ __launch_bounds__(64) void k_server(KParams<A> P, ServerBox *box,
     st[2] = __builtin_amdgcn_s_memrealtime();
     st[5] = __builtin_amdgcn_s_memtime();
 #endif
-    if (live) {
+    {
+      W *sc = (W *)stg[0];
+      if (live) {
+        const int base = pb * N + Gr::base(0, j);
 #pragma unroll
-      for (int k = 0; k < 16; k++) {
-        W v = x[k];
-        if (!A::kInvCanonical) v = P.ar.canon(v);
-        box->c[base + Gr::off(0, k)] = v;
+        for (int k = 0; k < 16; k++) {
+          W v = x[k];
+          if (!A::kInvCanonical) v = P.ar.canon(v);
+          sc[base + Gr::off(0, k)] = v;
+        }
       }
+      xsync<1>();
+      uint4 *gc = (uint4 *)box->c;
+      for (int i = lane; i < q4; i += 64) gc[i] = stg[0][i];
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // c reaches host memory before done
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -985,6 +1025,7 @@ __global__ __launch_bounds__(64) void k_server(KParams<A> P, ServerBox *box,
     __hip_atomic_store(&box->done, go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     seen = go;
     last = now;
+    xsync<1>();  // the next request's loads land in stg after every lane has stored c
   }
 }
 

@@ -65,12 +65,14 @@ hipError_t launch_fill(void *a, void *b, uint32_t logn, uint64_t q, uint64_t see
 // Mailbox of the small-transaction device server (k_server, nttmul.cpp Server): page-locked,
 // host-coherent memory shared by one host caller and one resident single-wave kernel -- the
 // MI355X form of the FPGA communicator's mode-3 GO + WaitForDoneAll polling
-// (NTT_PCIECommunicationv2.c:83-107, 211-215).  The host writes a, b, count, then go = seq; the
-// kernel (polling go) multiplies and writes c, then done = seq; stop asks it to leave.
+// (NTT_PCIECommunicationv2.c:83-107, 211-215).  The host writes a and b, then the go word
+// (seq << 8) | count; the kernel (polling go) multiplies, writes c, then done = that go word.
+// count 0 asks the kernel to leave (it acknowledges in done first).  One word carries the
+// sequence number and the product count, so the kernel learns both from one PCIe read.
 struct ServerBox {
   static constexpr int kWords = 1024;            // per operand: n x count <= 1024 words
+  static constexpr unsigned kStop = 0;           // count field of a stop request
   alignas(128) uint32_t go;
-  uint32_t count, stop;
   alignas(128) uint32_t done;
   alignas(128) uint32_t a[kWords];
   alignas(128) uint32_t b[kWords];
@@ -81,7 +83,7 @@ struct ServerBox {
 };
 // Launch the server for products of n = 2^logn <= 1024 u32 words (q < 2^31) on stream s; it
 // leaves after idle_ticks of the 100 MHz clock without a request, after life_ticks in all, or
-// when box->stop is set.  hipErrorNotSupported for other (n, q).
+// on a stop request.  hipErrorNotSupported for other (n, q).
 hipError_t launch_server(const LaunchTables &T, ServerBox *box, unsigned long long idle_ticks,
                          unsigned long long life_ticks, hipStream_t s);
 

@@ -524,10 +524,13 @@ int run_host_dev(nttmul_ctx *ctx, DevState &d, const HostJob &J, size_t p0, size
 int server_stop(nttmul_ctx *ctx) {
   Server &S = ctx->server;
   if (!S.running) return NTTMUL_OK;
-  __atomic_store_n(&S.box->stop, 1u, __ATOMIC_RELEASE);
+  // a stop request: a new sequence number with count 0 (the kernel acknowledges it in done)
+  __atomic_store_n(&S.box->go, ((++S.seq) << 8) | ServerBox::kStop, __ATOMIC_RELEASE);
   S.running = false;
   const hipError_t e = hipStreamSynchronize(S.s);
-  __atomic_store_n(&S.box->stop, 0u, __ATOMIC_RELEASE);
+  // (a kernel that had already left on its own never acknowledged: do it here, so a relaunched
+  // one starts idle instead of reading the stop request)
+  __atomic_store_n(&S.box->done, __atomic_load_n(&S.box->go, __ATOMIC_ACQUIRE), __ATOMIC_RELEASE);
   return e == hipSuccess ? NTTMUL_OK : fail(ctx, e, "device server exit");
 }
 
@@ -574,8 +577,7 @@ int run_server(nttmul_ctx *ctx, void *c, const void *a, const void *b, size_t ba
   }
   memcpy(S.box->a, a, words * 4);
   memcpy(S.box->b, b, words * 4);
-  S.box->count = (uint32_t)batch;
-  const unsigned seq = ++S.seq;
+  const unsigned seq = ((++S.seq) << 8) | (unsigned)batch;  // batch <= 4: one go word
   const auto t0 = std::chrono::steady_clock::now();
   __atomic_store_n(&S.box->go, seq, __ATOMIC_RELEASE);
   for (unsigned spin = 1; __atomic_load_n(&S.box->done, __ATOMIC_ACQUIRE) != seq; spin++) {
