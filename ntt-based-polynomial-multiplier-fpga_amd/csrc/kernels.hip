@@ -900,10 +900,14 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
   CLK_STAMP(1);
 }
 
+// s_sleep argument between the device server's polls (x 64 cycles: 16 = 0.43 us at 2.4 GHz)
+#ifndef NTTMUL_SERVER_POLL_SLEEP
+#define NTTMUL_SERVER_POLL_SLEEP 16
+#endif
 // Small-transaction device server (host calls of at most 1024 words per operand, e.g. the
 // reference's ntt256_product4 through the compat shims; nttmul.cpp Server).  One resident wave
-// polls the mailbox's go word (sequence number << 8 | product count) in host memory with two
-// system-scope reads in flight; on a new word it takes the request (system acquire), pulls a and
+// polls the mailbox's go word (sequence number << 8 | product count) in host memory with three
+// staggered system-scope reads in flight; on a new word it takes the request (system acquire), pulls a and
 // b from the mailbox in
 // 16-byte loads into LDS (every load a PCIe read: the whole request in as few, wide reads as
 // possible), runs the same fused product as k_rows (64 / (n / 16) products per wave, exchanges
@@ -931,20 +935,45 @@ __global__ __launch_bounds__(64) void k_server(KParams<A> P, ServerBox *box,
   seen = __builtin_amdgcn_readfirstlane(seen);
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   unsigned long long last = t0;
-  // two polls in flight: the next read of go is issued before the previous one is waited for,
-  // so a request is seen about half a PCIe round trip sooner than by one poll at a time
-  unsigned pend = __hip_atomic_load(&box->go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  // three polls in flight, issued NTTMUL_SERVER_POLL_SLEEP apart (about a third of a PCIe read
+  // round trip), each waited for only when two newer ones are out: a request is seen about a
+  // third of a round trip after it is posted plus the read's way back, instead of up to a whole
+  // round trip later (unrolled three times so no poll register is moved while its read is out)
+  constexpr int kSleep = NTTMUL_SERVER_POLL_SLEEP;
   for (;;) {
-    __builtin_amdgcn_s_sleep(1);
-    const unsigned next = __hip_atomic_load(&box->go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __builtin_amdgcn_sched_barrier(0);
-    const unsigned go = __builtin_amdgcn_readfirstlane(pend);
-    pend = next;
-    const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-    if (go == seen) {
-      if (now - last > idle_ticks || now - t0 > life_ticks) break;
-      continue;
+    unsigned go = seen;
+    {
+      const auto poll = [&]() {
+        const unsigned v = __hip_atomic_load(&box->go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_amdgcn_sched_barrier(0);
+        return v;
+      };
+      const auto idle = [&]() {
+        const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+        return now - last > idle_ticks || now - t0 > life_ticks;
+      };
+      unsigned p0 = poll();
+      __builtin_amdgcn_s_sleep(kSleep);
+      unsigned p1 = poll();
+      __builtin_amdgcn_s_sleep(kSleep);
+      bool quit = false;
+      for (;;) {
+        unsigned p2 = poll();
+        if ((go = __builtin_amdgcn_readfirstlane(p0)) != seen) break;
+        if ((quit = idle())) break;
+        __builtin_amdgcn_s_sleep(kSleep);
+        p0 = poll();
+        if ((go = __builtin_amdgcn_readfirstlane(p1)) != seen) break;
+        if ((quit = idle())) break;
+        __builtin_amdgcn_s_sleep(kSleep);
+        p1 = poll();
+        if ((go = __builtin_amdgcn_readfirstlane(p2)) != seen) break;
+        if ((quit = idle())) break;
+        __builtin_amdgcn_s_sleep(kSleep);
+      }
+      if (quit) break;
     }
+    const unsigned long long now = __builtin_amdgcn_s_memrealtime();
     const int count = (int)(go & 0xFFu);
     if (count == (int)ServerBox::kStop || count > PB) {  // stop (count > PB: never posted)
       __hip_atomic_store(&box->done, go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1419,13 +1448,13 @@ __device__ __forceinline__ void st_pol(T *p, T v) {
 __device__ __forceinline__ void mp_publish(unsigned *cnt) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 // the consuming workgroup's wait for `need` finished producer tasks
 __device__ __forceinline__ void mp_wait(const MpSync &S, const unsigned *cnt, unsigned need) {
   if (threadIdx.x == 0) {
     unsigned polls = 0;
-    while (__hip_atomic_load((unsigned *)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+    while (__hip_atomic_load((unsigned *)cnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < need) {
       __builtin_amdgcn_s_sleep(2);
       if (++polls == (1u << 20)) {  // >= 60 ms of polling: far beyond any correct wait
         __hip_atomic_store(S.fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1434,6 +1463,8 @@ __device__ __forceinline__ void mp_wait(const MpSync &S, const unsigned *cnt, un
     }
   }
   __syncthreads();
+  // the producers' stores, made visible by their release, before any lane of this workgroup loads
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
 
 __device__ __forceinline__ void mp_stat(const MpSync &S, int kind, unsigned long long t0,
@@ -1845,7 +1876,8 @@ static hipError_t multipass_persist(const LaunchTables &T, const void *a, const 
   S.head = sw;
   S.fault = sw + 1;
   S.cnt = sw + 2;
-  S.lag = (unsigned)T.mp_lag;
+  S.lag = (unsigned)(T.mp_lag < 4096 ? T.mp_lag : 4096);  // (batch + 2 lag) T stays far below 2^32
+  if ((batch + 2 * (size_t)S.lag) * (32 + (1u << L1)) >= (1ull << 31)) return hipErrorInvalidValue;
   S.stats = (unsigned long long *)T.mp_stats;
   const unsigned grid = (unsigned)(per_cu * (T.cus > 0 ? T.cus : 256));
   hipLaunchKernelGGL((k_mp_persist<A, IO, L1>), dim3(grid), dim3(256), 0, s, P, (const IO *)a,

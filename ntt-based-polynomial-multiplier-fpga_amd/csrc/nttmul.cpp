@@ -536,6 +536,8 @@ int server_stop(nttmul_ctx *ctx) {
 
 int server_launch(nttmul_ctx *ctx, DevState &d) {
   Server &S = ctx->server;
+  DeviceGuard guard;
+  HIP_TRY(ctx, hipSetDevice(d.id));
   HIP_TRY(ctx, launch_server(tables_for(ctx, d), S.dbox, kServerIdleTicks, kServerLifeTicks, S.s));
   S.running = true;
   S.launched = S.last_done = std::chrono::steady_clock::now();
@@ -559,8 +561,9 @@ int run_server(nttmul_ctx *ctx, void *c, const void *a, const void *b, size_t ba
   }
   Server &S = ctx->server;
   DevState &d = ctx->dev[0];
-  HIP_TRY(ctx, hipSetDevice(d.id));
   if (!S.box) {
+    DeviceGuard guard;
+    HIP_TRY(ctx, hipSetDevice(d.id));
     HIP_TRY(ctx, hipHostMalloc((void **)&S.box, sizeof(ServerBox), hipHostMallocCoherent));
     memset((void *)S.box, 0, sizeof(ServerBox));
     HIP_TRY(ctx, hipHostGetDevicePointer((void **)&S.dbox, S.box, 0));
@@ -616,11 +619,11 @@ int run_host(nttmul_ctx *ctx, int op, void *c, const void *a, const void *b, siz
   if (io_bits != 32 && io_bits != 64) return NTTMUL_EINVAL;
   if (io_bits == 32 && ctx->plan.q > 0xFFFFFFFFull) return NTTMUL_EINVAL;
   if (!batch) return NTTMUL_OK;
-  DeviceGuard guard;
-  if (op == OP_MULTIPLY && io_bits == 32) {
+  if (op == OP_MULTIPLY && io_bits == 32) {  // (no HIP call on the server's fast path)
     const int st = run_server(ctx, c, a, b, batch);
     if (st <= 0) return st;
   }
+  DeviceGuard guard;
   HostJob J;
   J.op = op;
   J.io_bits = io_bits;
