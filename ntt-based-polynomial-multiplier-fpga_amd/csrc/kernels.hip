@@ -911,8 +911,8 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
 // b from the mailbox in
 // 16-byte loads into LDS (every load a PCIe read: the whole request in as few, wide reads as
 // possible), runs the same fused product as k_rows (64 / (n / 16) products per wave, exchanges
-// ordered per wave), stages c in LDS and writes it back in 16-byte stores, releases (system) and
-// publishes done = the go word.  A single product of n <= 512 transforms a and b on two lane groups at
+// ordered per wave), stages c in LDS and writes it back in 16-byte stores (the host takes the
+// request as done when every word of c has changed from the pending marker).  A single product of n <= 512 transforms a and b on two lane groups at
 // once (each group one polynomial, b's result handed to a's lanes by lane permutes) instead of
 // both on one group.  It leaves on stop, after idle_ticks without a request or after life_ticks
 // in all (the host relaunches it on demand), so the wave always ends -- the FPGA's GO / done-all
@@ -975,10 +975,7 @@ __global__ __launch_bounds__(64) void k_server(KParams<A> P, ServerBox *box,
     }
     const unsigned long long now = __builtin_amdgcn_s_memrealtime();
     const int count = (int)(go & 0xFFu);
-    if (count == (int)ServerBox::kStop || count > PB) {  // stop (count > PB: never posted)
-      __hip_atomic_store(&box->done, go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      break;
-    }
+    if (count == (int)ServerBox::kStop || count > PB) break;  // stop (count > PB: never posted)
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the host's a, b before go
 #ifdef NTTMUL_CLOCK_STAMPS
     unsigned long long st[6];
@@ -1039,19 +1036,21 @@ __global__ __launch_bounds__(64) void k_server(KParams<A> P, ServerBox *box,
         }
       }
       xsync<1>();
+      // (the host watches c itself: a word that is no longer ServerBox::kPending has landed, so
+      // no release fence or done word is needed before polling again)
       uint4 *gc = (uint4 *)box->c;
       for (int i = lane; i < q4; i += 64) gc[i] = stg[0][i];
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // c reaches host memory before done
+#ifdef NTTMUL_CLOCK_STAMPS  // diagnostic build: c landed (fence), then the stamps, then done
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#ifdef NTTMUL_CLOCK_STAMPS
     st[3] = __builtin_amdgcn_s_memrealtime();
     if (threadIdx.x == 0)  // vector stores from lane 0, released with done below
       for (int k = 0; k < 6; k++) box->stamp[k] = st[k];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
     __hip_atomic_store(&box->done, go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
     seen = go;
     last = now;
     xsync<1>();  // the next request's loads land in stg after every lane has stored c

@@ -65,13 +65,16 @@ hipError_t launch_fill(void *a, void *b, uint32_t logn, uint64_t q, uint64_t see
 // Mailbox of the small-transaction device server (k_server, nttmul.cpp Server): page-locked,
 // host-coherent memory shared by one host caller and one resident single-wave kernel -- the
 // MI355X form of the FPGA communicator's mode-3 GO + WaitForDoneAll polling
-// (NTT_PCIECommunicationv2.c:83-107, 211-215).  The host writes a and b, then the go word
-// (seq << 8) | count; the kernel (polling go) multiplies, writes c, then done = that go word.
-// count 0 asks the kernel to leave (it acknowledges in done first).  One word carries the
-// sequence number and the product count, so the kernel learns both from one PCIe read.
+// (NTT_PCIECommunicationv2.c:83-107, 211-215).  The host sets c to kPending, writes a and b,
+// then the go word (seq << 8) | count; the kernel (polling go) multiplies and writes c, and the
+// request is complete when no word of c is kPending.  One word carries the sequence number and
+// the product count, so the kernel learns both from one PCIe read; count 0 asks it to leave.
+// done is the last go word already served: written by the host before each launch (the kernel
+// starts from it) and, in the diagnostic build, by the kernel after its stamps.
 struct ServerBox {
   static constexpr int kWords = 1024;            // per operand: n x count <= 1024 words
   static constexpr unsigned kStop = 0;           // count field of a stop request
+  static constexpr uint32_t kPending = 0xFFFFFFFFu;  // no canonical coefficient (q < 2^31)
   alignas(128) uint32_t go;
   alignas(128) uint32_t done;
   alignas(128) uint32_t a[kWords];

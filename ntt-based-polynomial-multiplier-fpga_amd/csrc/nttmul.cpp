@@ -81,7 +81,8 @@ struct Server {
   ServerBox *box = nullptr;
   ServerBox *dbox = nullptr;                  // the mailbox as a device pointer
   hipStream_t s = nullptr;
-  unsigned seq = 0;                           // last request posted
+  unsigned seq = 0;                           // sequence number of the last go word posted
+  unsigned served = 0;                        // the last go word whose product was received
   uint64_t host_ns = 0;                       // go -> done seen on the host, last request
   bool running = false;                       // launched and not known to have left
   std::chrono::steady_clock::time_point launched, last_done;
@@ -524,18 +525,20 @@ int run_host_dev(nttmul_ctx *ctx, DevState &d, const HostJob &J, size_t p0, size
 int server_stop(nttmul_ctx *ctx) {
   Server &S = ctx->server;
   if (!S.running) return NTTMUL_OK;
-  // a stop request: a new sequence number with count 0 (the kernel acknowledges it in done)
+  // a stop request: a new sequence number with count 0
   __atomic_store_n(&S.box->go, ((++S.seq) << 8) | ServerBox::kStop, __ATOMIC_RELEASE);
   S.running = false;
   const hipError_t e = hipStreamSynchronize(S.s);
-  // (a kernel that had already left on its own never acknowledged: do it here, so a relaunched
-  // one starts idle instead of reading the stop request)
-  __atomic_store_n(&S.box->done, __atomic_load_n(&S.box->go, __ATOMIC_ACQUIRE), __ATOMIC_RELEASE);
+  // (the stop needs no answer: a relaunched kernel starts from done = S.served, and the next
+  // request's go differs from both)
+  __atomic_store_n(&S.box->go, S.served, __ATOMIC_RELEASE);
   return e == hipSuccess ? NTTMUL_OK : fail(ctx, e, "device server exit");
 }
 
 int server_launch(nttmul_ctx *ctx, DevState &d) {
   Server &S = ctx->server;
+  // the kernel starts from done: the last request it must not serve again (no kernel runs now)
+  __atomic_store_n(&S.box->done, S.served, __ATOMIC_RELEASE);
   DeviceGuard guard;
   HIP_TRY(ctx, hipSetDevice(d.id));
   HIP_TRY(ctx, launch_server(tables_for(ctx, d), S.dbox, kServerIdleTicks, kServerLifeTicks, S.s));
@@ -578,16 +581,34 @@ int run_server(nttmul_ctx *ctx, void *c, const void *a, const void *b, size_t ba
     const int st = server_launch(ctx, d);
     if (st) return st;
   }
+  // Completion is the result itself: c is set to a word no product can hold (the server's
+  // q < 2^31, so 0xFFFFFFFF) before go, and the request is done when no word of c still holds it.
+  // Every 4-byte store of the kernel lands whole, so this needs no release fence and no done word
+  // on the device side (one PCIe write round trip less per request).
+  uint32_t *bc = S.box->c;
+  for (size_t i = 0; i < words; i++) bc[i] = ServerBox::kPending;
   memcpy(S.box->a, a, words * 4);
   memcpy(S.box->b, b, words * 4);
   const unsigned seq = ((++S.seq) << 8) | (unsigned)batch;  // batch <= 4: one go word
   const auto t0 = std::chrono::steady_clock::now();
   __atomic_store_n(&S.box->go, seq, __ATOMIC_RELEASE);
-  for (unsigned spin = 1; __atomic_load_n(&S.box->done, __ATOMIC_ACQUIRE) != seq; spin++) {
+  const auto landed = [&]() {
+    for (size_t i = 0; i < words; i++)
+      if (__atomic_load_n(bc + i, __ATOMIC_RELAXED) == ServerBox::kPending) return false;
+    std::atomic_thread_fence(std::memory_order_acquire);
+#ifdef NTTMUL_CLOCK_STAMPS  // (the diagnostic build's stamps are released with done)
+    if (__atomic_load_n(&S.box->done, __ATOMIC_ACQUIRE) != seq) return false;
+#endif
+    return true;
+  };
+  for (unsigned spin = 1; !landed(); spin++) {
     __builtin_ia32_pause();
-    if (spin % 4096) continue;
+    if (spin % 1024) continue;
     const hipError_t q = hipStreamQuery(S.s);
-    if (q == hipSuccess) {           // the kernel left before it saw this request: relaunch
+    if (q == hipSuccess) {
+      // the kernel has left, and a finished kernel's stores have all landed: either it served
+      // this request after the check above, or it left before it saw it -- then relaunch
+      if (landed()) break;
       S.running = false;
       const int st = server_launch(ctx, d);
       if (st) return st;
@@ -601,9 +622,10 @@ int run_server(nttmul_ctx *ctx, void *c, const void *a, const void *b, size_t ba
       return NTTMUL_EHIP;
     }
   }
+  S.served = seq;
   S.last_done = std::chrono::steady_clock::now();
   S.host_ns = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(S.last_done - t0).count();
-  memcpy(c, S.box->c, words * 4);
+  memcpy(c, bc, words * 4);
   ctx->last_path = 3;
   return NTTMUL_OK;
 }
