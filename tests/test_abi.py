@@ -23,6 +23,23 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, s), s
 
 
+def test_diag_library_exports_both_headers():
+    """lib/libnttmul_diag.so (include/nttmul_diag.h) is the same ABI plus the diagnostic entry
+    points: every symbol of both headers, unmangled."""
+    import re
+    path = os.path.join(os.path.dirname(nttmul.LIB_PATH), "libnttmul_diag.so")
+    if not os.path.exists(path):
+        pytest.skip("diagnostic build not present")
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True,
+                         check=True).stdout
+    names = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    diag_h = os.path.join(os.path.dirname(nttmul.HEADER_PATH), "nttmul_diag.h")
+    diag = set(re.findall(r"^int (nttmul_diag_\w+)\(", open(diag_h).read(), re.M))
+    assert diag == {"nttmul_diag_clock_stamps", "nttmul_diag_server_stamps"}, diag
+    missing = (set(nttmul.exported_symbols()) | diag) - names
+    assert not missing, missing
+
+
 def test_exports_are_plain_c_abi():
     out = subprocess.run(["nm", "-D", "--defined-only", nttmul.LIB_PATH], capture_output=True,
                          text=True, check=True).stdout
