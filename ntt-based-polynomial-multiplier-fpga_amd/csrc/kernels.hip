@@ -900,26 +900,28 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
   CLK_STAMP(1);
 }
 
-// s_sleep argument between the device server's polls (x 64 cycles: 16 = 0.43 us at 2.4 GHz)
+// s_sleep argument between the device server's polls (x 64 cycles: 2 = 53 ns at 2.4 GHz)
 #ifndef NTTMUL_SERVER_POLL_SLEEP
-#define NTTMUL_SERVER_POLL_SLEEP 16
+#define NTTMUL_SERVER_POLL_SLEEP 2
 #endif
 // Small-transaction device server (host calls of at most 1024 words per operand, e.g. the
 // reference's ntt256_product4 through the compat shims; nttmul.cpp Server).  One resident wave
-// polls the mailbox's go word (sequence number << 8 | product count) in host memory with three
-// staggered system-scope reads in flight; on a new word it takes the request (system acquire), pulls a and
-// b from the mailbox in
-// 16-byte loads into LDS (every load a PCIe read: the whole request in as few, wide reads as
-// possible), runs the same fused product as k_rows (64 / (n / 16) products per wave, exchanges
-// ordered per wave), stages c in LDS and writes it back in 16-byte stores (the host takes the
-// request as done when every word of c has changed from the pending marker).  A single product of n <= 512 transforms a and b on two lane groups at
-// once (each group one polynomial, b's result handed to a's lanes by lane permutes) instead of
-// both on one group.  It leaves on stop, after idle_ticks without a request or after life_ticks
-// in all (the host relaunches it on demand), so the wave always ends -- the FPGA's GO / done-all
-// handshake without a kernel launch per call.
+// polls the request's go word (sequence number << 8 | product count) with system-scope reads;
+// on a new word it takes the request (system acquire), pulls a and
+// b in 16-byte system-scope loads into LDS, runs the same fused product as k_rows (64 / (n / 16)
+// products per wave, exchanges ordered per wave) on twiddles it copied into LDS at entry (no
+// L2 / HBM latency inside the transforms), stages c in LDS and writes it back in 16-byte stores
+// (the host takes the request as done when every word of c has changed from the pending
+// marker).  The request half of the mailbox (req) is device memory the host writes through its
+// BAR mapping, so polls and operand loads stay on the device; c goes to host memory
+// (launch.hpp ServerReq / ServerBox).  A single product of n <= 512 transforms a and b on two lane
+// groups at once (each group one polynomial, b's result handed to a's lanes by lane permutes)
+// instead of both on one group.  It leaves on stop, after idle_ticks without a request or after
+// life_ticks in all (the host relaunches it on demand), so the wave always ends -- the FPGA's
+// GO / done-all handshake without a kernel launch per call.
 template <class A, int LOGS>
-__global__ __launch_bounds__(64) void k_server(KParams<A> P, ServerBox *box,
-                                               unsigned long long idle_ticks,
+__global__ __launch_bounds__(64) void k_server(KParams<A> P, const ServerReq *req, ServerBox *box,
+                                               unsigned tw_pairs, unsigned long long idle_ticks,
                                                unsigned long long life_ticks) {
   using W = typename A::word;
   using Gr = Groups<LOGS, kWT<A, LOGS>()>;
@@ -928,51 +930,38 @@ __global__ __launch_bounds__(64) void k_server(KParams<A> P, ServerBox *box,
   constexpr int KW = ServerBox::kWords;
   __shared__ W lds[PB][NP];
   __shared__ uint4 stg[2][KW / 4];  // a, b as loaded (c as stored reuses stg[0])
+  __shared__ TwPair<W> twf[2 * N], twi[2 * N];  // launch_server: tw_pairs <= 2n
   const int lane = threadIdx.x, pb = lane / TP, j = lane % TP;
+  for (unsigned i = lane; i < tw_pairs; i += 64) {
+    twf[i] = P.fw[i];
+    twi[i] = P.iw[i];
+  }
+  P.fw = twf;
+  P.iw = twi;
   W *lx = lds[pb];
   constexpr int D = NTTMUL_BASE_D ? A::kBaseD : 0;
   unsigned seen = __hip_atomic_load(&box->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   seen = __builtin_amdgcn_readfirstlane(seen);
+  xsync<1>();  // the twiddles in LDS before the first transform
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   unsigned long long last = t0;
-  // three polls in flight, issued NTTMUL_SERVER_POLL_SLEEP apart (about a third of a PCIe read
-  // round trip), each waited for only when two newer ones are out: a request is seen about a
-  // third of a round trip after it is posted plus the read's way back, instead of up to a whole
-  // round trip later (unrolled three times so no poll register is moved while its read is out)
+  // one poll at a time, NTTMUL_SERVER_POLL_SLEEP apart.  (Rounds 4b-4f kept three polls in
+  // flight 16 x 64 cycles apart, sized for reads across PCIe; with the request in device memory a
+  // single poll is 1 us faster per request, and with it in host memory too:
+  // tools/microbench/mailbox_latency.hip, profiles/r4/r4g/mailbox_latency.json)
   constexpr int kSleep = NTTMUL_SERVER_POLL_SLEEP;
   for (;;) {
     unsigned go = seen;
-    {
-      const auto poll = [&]() {
-        const unsigned v = __hip_atomic_load(&box->go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __builtin_amdgcn_sched_barrier(0);
-        return v;
-      };
-      const auto idle = [&]() {
-        const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-        return now - last > idle_ticks || now - t0 > life_ticks;
-      };
-      unsigned p0 = poll();
+    bool quit = false;
+    for (;;) {
+      go = __builtin_amdgcn_readfirstlane(
+          __hip_atomic_load(&req->go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+      if (go != seen) break;
+      const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+      if ((quit = now - last > idle_ticks || now - t0 > life_ticks)) break;
       __builtin_amdgcn_s_sleep(kSleep);
-      unsigned p1 = poll();
-      __builtin_amdgcn_s_sleep(kSleep);
-      bool quit = false;
-      for (;;) {
-        unsigned p2 = poll();
-        if ((go = __builtin_amdgcn_readfirstlane(p0)) != seen) break;
-        if ((quit = idle())) break;
-        __builtin_amdgcn_s_sleep(kSleep);
-        p0 = poll();
-        if ((go = __builtin_amdgcn_readfirstlane(p1)) != seen) break;
-        if ((quit = idle())) break;
-        __builtin_amdgcn_s_sleep(kSleep);
-        p1 = poll();
-        if ((go = __builtin_amdgcn_readfirstlane(p2)) != seen) break;
-        if ((quit = idle())) break;
-        __builtin_amdgcn_s_sleep(kSleep);
-      }
-      if (quit) break;
     }
+    if (quit) break;
     const unsigned long long now = __builtin_amdgcn_s_memrealtime();
     const int count = (int)(go & 0xFFu);
     if (count == (int)ServerBox::kStop || count > PB) break;  // stop (count > PB: never posted)
@@ -982,11 +971,13 @@ __global__ __launch_bounds__(64) void k_server(KParams<A> P, ServerBox *box,
     st[0] = __builtin_amdgcn_s_memrealtime();
 #endif
     const int q4 = count * (N / 4);  // 16-byte quads per operand (count <= PB, so <= KW / 4)
-    {
-      const uint4 *ga = (const uint4 *)box->a, *gb = (const uint4 *)box->b;
+    {  // system-scope (sc0 sc1) loads: the host's writes reach memory behind any cached copy
+      const auto ra = span_rsrc(req->a, KW), rb = span_rsrc(req->b, KW);
       for (int i = lane; i < q4; i += 64) {
-        stg[0][i] = ga[i];
-        stg[1][i] = gb[i];
+        const auto va = __builtin_amdgcn_raw_buffer_load_b128(ra, i * 16, 0, 17);
+        const auto vb = __builtin_amdgcn_raw_buffer_load_b128(rb, i * 16, 0, 17);
+        stg[0][i] = make_uint4(va[0], va[1], va[2], va[3]);
+        stg[1][i] = make_uint4(vb[0], vb[1], vb[2], vb[3]);
       }
     }
     xsync<1>();
@@ -1978,15 +1969,19 @@ static hipError_t launch_polymul_(const LaunchTables &T, const void *a, const vo
 #endif
 }
 
-hipError_t launch_server(const LaunchTables &T, ServerBox *box, unsigned long long idle_ticks,
-                         unsigned long long life_ticks, hipStream_t s) {
-  if (T.word_bits != 32 || a32_kind(T.q) != A32Kind::Plantard || T.logn < 8 || T.logn > 10)
+hipError_t launch_server(const LaunchTables &T, const ServerReq *req, ServerBox *box,
+                         unsigned long long idle_ticks, unsigned long long life_ticks,
+                         hipStream_t s) {
+  const size_t pairs = T.tw_bytes / sizeof(TwPair<uint32_t>);
+  if (T.word_bits != 32 || a32_kind(T.q) != A32Kind::Plantard || T.logn < 8 || T.logn > 10 ||
+      pairs > (2u << T.logn))
     return hipErrorNotSupported;
   const KParams<Arith32P> P = product_params<Arith32P>(T);
+  const unsigned tp = (unsigned)pairs;
   switch (T.logn) {
-    case 8: hipLaunchKernelGGL((k_server<Arith32P, 8>), dim3(1), dim3(64), 0, s, P, box, idle_ticks, life_ticks); break;
-    case 9: hipLaunchKernelGGL((k_server<Arith32P, 9>), dim3(1), dim3(64), 0, s, P, box, idle_ticks, life_ticks); break;
-    default: hipLaunchKernelGGL((k_server<Arith32P, 10>), dim3(1), dim3(64), 0, s, P, box, idle_ticks, life_ticks); break;
+    case 8: hipLaunchKernelGGL((k_server<Arith32P, 8>), dim3(1), dim3(64), 0, s, P, req, box, tp, idle_ticks, life_ticks); break;
+    case 9: hipLaunchKernelGGL((k_server<Arith32P, 9>), dim3(1), dim3(64), 0, s, P, req, box, tp, idle_ticks, life_ticks); break;
+    default: hipLaunchKernelGGL((k_server<Arith32P, 10>), dim3(1), dim3(64), 0, s, P, req, box, tp, idle_ticks, life_ticks); break;
   }
   return hipGetLastError();
 }

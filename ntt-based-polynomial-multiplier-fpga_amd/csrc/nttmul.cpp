@@ -11,6 +11,7 @@
 // and provides the software path's entry points (ntt256_product1/4, NTT/ntt256.h:85-86) as
 // compat shims.  There is no CPU fallback anywhere in this library.
 #include <hip/hip_runtime.h>
+#include <hsa/hsa_ext_amd.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -75,11 +76,15 @@ struct DevState {
   std::atomic<uintptr_t> prod_s{0};  // (uintptr_t)stream | 1 (the null stream is a stream too); 0: none
 };
 
-// The small-transaction device server (kernels.hip k_server): its mailbox in page-locked,
-// host-coherent memory and the stream its resident kernel runs on.
+// The small-transaction device server (kernels.hip k_server): its mailbox (launch.hpp: the
+// request half in host-mapped device memory, the result half in page-locked host memory) and the
+// stream its resident kernel runs on.
 struct Server {
+  ServerReq *req = nullptr;                   // the request half as the host writes it
+  ServerReq *dreq = nullptr;                  // ... as the kernel reads it
+  bool req_in_vram = false;                   // (false: pinned host memory, req == host pointer)
   ServerBox *box = nullptr;
-  ServerBox *dbox = nullptr;                  // the mailbox as a device pointer
+  ServerBox *dbox = nullptr;                  // the result half as a device pointer
   hipStream_t s = nullptr;
   unsigned seq = 0;                           // sequence number of the last go word posted
   unsigned served = 0;                        // the last go word whose product was received
@@ -156,6 +161,7 @@ LaunchTables tables_for(const nttmul_ctx *ctx, const DevState &d) {
   T.fi = P.fi; T.fis = P.fis; T.wfi = P.wfi; T.wfis = P.wfis; T.r2 = P.r2;
   T.fw = d.fw;
   T.iw = d.iw;
+  T.tw_bytes = P.fw.size();
   T.cus = d.cus;
   T.prio = ctx->issue_prio;
   return T;
@@ -522,16 +528,24 @@ int run_host_dev(nttmul_ctx *ctx, DevState &d, const HostJob &J, size_t p0, size
 // the resident kernel is (re)launched when it is not known to be alive: never launched, idle on
 // the host's clock for longer than kServerIdleHost (it leaves after 20 ms on its own), older than
 // kServerLifeHost, or found finished while a request waits.  Every spin is bounded.
+// The go word into the request half.  A BAR mapping of device memory is uncached or
+// write-combining on the host, so the fences keep a and b ahead of go and push go out at once.
+void post_go(Server &S, unsigned v) {
+  __builtin_ia32_sfence();
+  __atomic_store_n(&S.req->go, v, __ATOMIC_RELEASE);
+  __builtin_ia32_sfence();
+}
+
 int server_stop(nttmul_ctx *ctx) {
   Server &S = ctx->server;
   if (!S.running) return NTTMUL_OK;
   // a stop request: a new sequence number with count 0
-  __atomic_store_n(&S.box->go, ((++S.seq) << 8) | ServerBox::kStop, __ATOMIC_RELEASE);
+  post_go(S, ((++S.seq) << 8) | ServerBox::kStop);
   S.running = false;
   const hipError_t e = hipStreamSynchronize(S.s);
   // (the stop needs no answer: a relaunched kernel starts from done = S.served, and the next
   // request's go differs from both)
-  __atomic_store_n(&S.box->go, S.served, __ATOMIC_RELEASE);
+  post_go(S, S.served);
   return e == hipSuccess ? NTTMUL_OK : fail(ctx, e, "device server exit");
 }
 
@@ -541,9 +555,55 @@ int server_launch(nttmul_ctx *ctx, DevState &d) {
   __atomic_store_n(&S.box->done, S.served, __ATOMIC_RELEASE);
   DeviceGuard guard;
   HIP_TRY(ctx, hipSetDevice(d.id));
-  HIP_TRY(ctx, launch_server(tables_for(ctx, d), S.dbox, kServerIdleTicks, kServerLifeTicks, S.s));
+  HIP_TRY(ctx, launch_server(tables_for(ctx, d), S.dreq, S.dbox, kServerIdleTicks,
+                             kServerLifeTicks, S.s));
   S.running = true;
   S.launched = S.last_done = std::chrono::steady_clock::now();
+  return NTTMUL_OK;
+}
+
+// The mailbox (launch.hpp ServerReq / ServerBox).  The request half goes to fine-grained device
+// memory when the runtime gives the host a mapping of it (large BAR) and a probe written through
+// that mapping reads back through the device; otherwise to pinned host memory.
+int server_alloc(nttmul_ctx *ctx, DevState &d) {
+  Server &S = ctx->server;
+  DeviceGuard guard;
+  HIP_TRY(ctx, hipSetDevice(d.id));
+  if (!S.box) {
+    HIP_TRY(ctx, hipHostMalloc((void **)&S.box, sizeof(ServerBox), hipHostMallocCoherent));
+    memset((void *)S.box, 0, sizeof(ServerBox));
+    HIP_TRY(ctx, hipHostGetDevicePointer((void **)&S.dbox, S.box, 0));
+  }
+  if (!S.s) HIP_TRY(ctx, hipStreamCreateWithFlags(&S.s, hipStreamNonBlocking));
+  void *dv = nullptr;
+  if (hipExtMallocWithFlags(&dv, sizeof(ServerReq), hipDeviceMallocFinegrained) == hipSuccess) {
+    hsa_amd_pointer_info_t info;
+    memset(&info, 0, sizeof(info));
+    info.size = sizeof(info);
+    ServerReq *hv = nullptr;
+    if (hsa_amd_pointer_info(dv, &info, nullptr, nullptr, nullptr) == HSA_STATUS_SUCCESS &&
+        info.hostBaseAddress && info.agentBaseAddress == dv)
+      hv = (ServerReq *)info.hostBaseAddress;
+    uint32_t back = 0;
+    if (hv) {
+      __atomic_store_n(&hv->go, 0x5A5A5A5Au, __ATOMIC_RELEASE);
+      __builtin_ia32_sfence();
+      if (hipMemcpy(&back, &((ServerReq *)dv)->go, 4, hipMemcpyDeviceToHost) != hipSuccess) back = 0;
+    }
+    if (back == 0x5A5A5A5Au) {
+      S.req = hv;
+      S.dreq = (ServerReq *)dv;
+      S.req_in_vram = true;
+    } else {
+      (void)hipFree(dv);
+    }
+  }
+  (void)hipGetLastError();
+  if (!S.req) {
+    HIP_TRY(ctx, hipHostMalloc((void **)&S.req, sizeof(ServerReq), hipHostMallocCoherent));
+    HIP_TRY(ctx, hipHostGetDevicePointer((void **)&S.dreq, S.req, 0));
+  }
+  post_go(S, 0);
   return NTTMUL_OK;
 }
 
@@ -564,13 +624,9 @@ int run_server(nttmul_ctx *ctx, void *c, const void *a, const void *b, size_t ba
   }
   Server &S = ctx->server;
   DevState &d = ctx->dev[0];
-  if (!S.box) {
-    DeviceGuard guard;
-    HIP_TRY(ctx, hipSetDevice(d.id));
-    HIP_TRY(ctx, hipHostMalloc((void **)&S.box, sizeof(ServerBox), hipHostMallocCoherent));
-    memset((void *)S.box, 0, sizeof(ServerBox));
-    HIP_TRY(ctx, hipHostGetDevicePointer((void **)&S.dbox, S.box, 0));
-    HIP_TRY(ctx, hipStreamCreateWithFlags(&S.s, hipStreamNonBlocking));
+  if (!S.req) {
+    const int st = server_alloc(ctx, d);
+    if (st) return st;
   }
   const auto now = std::chrono::steady_clock::now();
   if (S.running && (now - S.last_done > kServerIdleHost || now - S.launched > kServerLifeHost)) {
@@ -587,11 +643,11 @@ int run_server(nttmul_ctx *ctx, void *c, const void *a, const void *b, size_t ba
   // on the device side (one PCIe write round trip less per request).
   uint32_t *bc = S.box->c;
   for (size_t i = 0; i < words; i++) bc[i] = ServerBox::kPending;
-  memcpy(S.box->a, a, words * 4);
-  memcpy(S.box->b, b, words * 4);
+  memcpy(S.req->a, a, words * 4);
+  memcpy(S.req->b, b, words * 4);
   const unsigned seq = ((++S.seq) << 8) | (unsigned)batch;  // batch <= 4: one go word
   const auto t0 = std::chrono::steady_clock::now();
-  __atomic_store_n(&S.box->go, seq, __ATOMIC_RELEASE);
+  post_go(S, seq);
   const auto landed = [&]() {
     for (size_t i = 0; i < words; i++)
       if (__atomic_load_n(bc + i, __ATOMIC_RELAXED) == ServerBox::kPending) return false;
@@ -798,11 +854,16 @@ int nttmul_create(nttmul_ctx **ctx, uint32_t n, uint64_t q, int ndev) {
 void nttmul_destroy(nttmul_ctx *ctx) {
   if (!ctx) return;
   DeviceGuard guard;
-  if (ctx->server.box) {
+  Server &S = ctx->server;
+  if (S.box || S.req) {
     (void)hipSetDevice(ctx->dev[0].id);
     (void)server_stop(ctx);
-    if (ctx->server.s) (void)hipStreamDestroy(ctx->server.s);
-    (void)hipHostFree(ctx->server.box);
+    if (S.s) (void)hipStreamDestroy(S.s);
+    if (S.box) (void)hipHostFree(S.box);
+    if (S.req_in_vram)
+      (void)hipFree(S.dreq);
+    else if (S.req)
+      (void)hipHostFree(S.req);
   }
   for (int i = 0; i < ctx->ndev; i++) {
     DevState &d = ctx->dev[i];
