@@ -904,37 +904,152 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
 #ifndef NTTMUL_SERVER_POLL_SLEEP
 #define NTTMUL_SERVER_POLL_SLEEP 2
 #endif
+// The wide single-product path of the device server (n = 256, one product: every call of the
+// reference's ntt256_product4 / product1 shims).  The one-wave path gives a product 16 lanes of
+// 16 coefficients (a and b on two lane groups, the inverse on one), so a call is about 1,100
+// dependent VALU instructions on one SIMD; here each polynomial is a whole wave of 4
+// coefficients per lane: wave 0 transforms a while wave 1 transforms b, and wave 0 runs the base
+// multiplication and the inverse, about 3x fewer instructions on the critical path for 7 LDS
+// exchanges instead of 2.  Register groups of two stages: layout P holds element bits P, P + 1 in
+// the four registers, e = (t mod 2^P) | (t >> P) << (P + 2) | i << P for lane t, register i.
+// Types as in the fused product (Arith32P, NTTMUL_P_TYPED 2), with the planner's twiddle table
+// re-typed per entry in LDS (fu: every pair unsigned, fs: every pair signed) because the group
+// boundaries differ: the second stage of a group multiplies the first stage's differences as
+// signed values with signed pairs (odd entries), the first reads unsigned lazy values, and the
+// last forward stage leaves its differences signed for the base multiplication.
+template <int P_>
+__device__ __forceinline__ int wl_elem(int t, int i) {
+  return (t & ((1 << P_) - 1)) | ((t >> P_) << (P_ + 2)) | (i << P_);
+}
+__device__ __forceinline__ int wl_pad(int e) { return e + (e >> 5); }
+// one wave's four registers from layout PF to layout PT through its LDS region
+template <int PF, int PT>
+__device__ __forceinline__ void wl_exchange(uint32_t (&x)[4], uint32_t *lx, int t) {
+#pragma unroll
+  for (int i = 0; i < 4; i++) lx[wl_pad(wl_elem<PF>(t, i))] = x[i];
+  xsync<1>();
+#pragma unroll
+  for (int i = 0; i < 4; i++) x[i] = lx[wl_pad(wl_elem<PT>(t, i))];
+  xsync<1>();
+}
+// forward CT, stages 0-5 of the incomplete transform (D = 2), X canonical on entry (the API
+// contract); leaves layout 2 (element bits 2, 3 in the registers)
+__device__ __forceinline__ void wide_fwd(const Arith32P &ar, uint32_t (&x)[4],
+                                         const TwPair<uint32_t> *fu, const TwPair<uint32_t> *fs,
+                                         uint32_t *lx, int t) {
+  {  // stage 0 (d 128: register bit 1), entry 1
+    const TwPair<uint32_t> w = fu[1];
+    ar.template ct<true, false, true>(x[0], x[2], w.w, w.ws);
+    ar.template ct<true, false, true>(x[1], x[3], w.w, w.ws);
+  }
+  {  // stage 1 (d 64: register bit 0), entries 2 (sums) and 3 (differences)
+    const TwPair<uint32_t> w0 = fu[2], w1 = fs[3];
+    ar.template ct<false, false, false>(x[0], x[1], w0.w, w0.ws);
+    ar.template ct<false, true, false>(x[2], x[3], w1.w, w1.ws);
+  }
+  wl_exchange<6, 4>(x, lx, t);
+  {  // stage 2 (d 32: register bit 1), entry 4 + e >> 6
+    const TwPair<uint32_t> w = fu[4 + (t >> 4)];
+    ar.template ct<false, false, true>(x[0], x[2], w.w, w.ws);
+    ar.template ct<false, false, true>(x[1], x[3], w.w, w.ws);
+  }
+  {  // stage 3 (d 16: register bit 0), entry 8 + e >> 5
+    const int k = 8 + ((t >> 4) << 1);
+    const TwPair<uint32_t> w0 = fu[k], w1 = fs[k + 1];
+    ar.template ct<false, false, false>(x[0], x[1], w0.w, w0.ws);
+    ar.template ct<false, true, false>(x[2], x[3], w1.w, w1.ws);
+  }
+  wl_exchange<4, 2>(x, lx, t);
+  {  // stage 4 (d 8: register bit 1), entry 16 + e >> 4
+    const TwPair<uint32_t> w = fu[16 + (t >> 2)];
+    ar.template ct<false, false, true>(x[0], x[2], w.w, w.ws);
+    ar.template ct<false, false, true>(x[1], x[3], w.w, w.ws);
+  }
+  {  // stage 5 (d 4: register bit 0), entry 32 + e >> 3; differences stay signed
+    const int k = 32 + ((t >> 2) << 1);
+    const TwPair<uint32_t> w0 = fu[k], w1 = fs[k + 1];
+    ar.template ct<false, false, true>(x[0], x[1], w0.w, w0.ws);
+    ar.template ct<false, true, true>(x[2], x[3], w1.w, w1.ws);
+  }
+}
+// inverse GS from layout 2 (the first D = 2 stages are the base multiplication's), F folded into
+// stage 0; leaves layout 6 (e = t + 64 i), canonical
+__device__ __forceinline__ void wide_inv(const KParams<Arith32P> &P, uint32_t (&x)[4],
+                                         const TwPair<uint32_t> *iw, uint32_t *lx, int t) {
+  {  // stage 5 (register bit 0), entry 32 + e >> 3
+    const int k = 32 + ((t >> 2) << 1);
+    const TwPair<uint32_t> w0 = iw[k], w1 = iw[k + 1];
+    P.ar.gs(x[0], x[1], w0.w, w0.ws);
+    P.ar.gs(x[2], x[3], w1.w, w1.ws);
+  }
+  {  // stage 4 (register bit 1), entry 16 + e >> 4
+    const TwPair<uint32_t> w = iw[16 + (t >> 2)];
+    P.ar.gs(x[0], x[2], w.w, w.ws);
+    P.ar.gs(x[1], x[3], w.w, w.ws);
+  }
+  wl_exchange<2, 4>(x, lx, t);
+  {  // stage 3 (register bit 0), entry 8 + e >> 5
+    const int k = 8 + ((t >> 4) << 1);
+    const TwPair<uint32_t> w0 = iw[k], w1 = iw[k + 1];
+    P.ar.gs(x[0], x[1], w0.w, w0.ws);
+    P.ar.gs(x[2], x[3], w1.w, w1.ws);
+  }
+  {  // stage 2 (register bit 1), entry 4 + e >> 6
+    const TwPair<uint32_t> w = iw[4 + (t >> 4)];
+    P.ar.gs(x[0], x[2], w.w, w.ws);
+    P.ar.gs(x[1], x[3], w.w, w.ws);
+  }
+  wl_exchange<4, 6>(x, lx, t);
+  {  // stage 1 (register bit 0), entries 2 and 3
+    const TwPair<uint32_t> w0 = iw[2], w1 = iw[3];
+    P.ar.gs(x[0], x[1], w0.w, w0.ws);
+    P.ar.gs(x[2], x[3], w1.w, w1.ws);
+  }
+  // stage 0 (register bit 1) with F
+  P.ar.gs_scaled(x[0], x[2], P.f, P.fs, P.wf, P.wfs);
+  P.ar.gs_scaled(x[1], x[3], P.f, P.fs, P.wf, P.wfs);
+}
+
 // Small-transaction device server (host calls of at most 1024 words per operand, e.g. the
-// reference's ntt256_product4 through the compat shims; nttmul.cpp Server).  One resident wave
-// polls the request's go word (sequence number << 8 | product count) with system-scope reads;
-// on a new word it takes the request (system acquire), pulls a and
-// b in 16-byte system-scope loads into LDS, runs the same fused product as k_rows (64 / (n / 16)
-// products per wave, exchanges ordered per wave) on twiddles it copied into LDS at entry (no
-// L2 / HBM latency inside the transforms), stages c in LDS and writes it back in 16-byte stores
-// (the host takes the request as done when every word of c has changed from the pending
-// marker).  The request half of the mailbox (req) is device memory the host writes through its
-// BAR mapping, so polls and operand loads stay on the device; c goes to host memory
-// (launch.hpp ServerReq / ServerBox).  A single product of n <= 512 transforms a and b on two lane
-// groups at once (each group one polynomial, b's result handed to a's lanes by lane permutes)
-// instead of both on one group.  It leaves on stop, after idle_ticks without a request or after
-// life_ticks in all (the host relaunches it on demand), so the wave always ends -- the FPGA's
-// GO / done-all handshake without a kernel launch per call.
+// reference's ntt256_product4 through the compat shims; nttmul.cpp Server).  Wave 0 polls the
+// request's go word (sequence number << 8 | product count) with system-scope reads; on a new word
+// it takes the request (system acquire), pulls a and b in system-scope loads, runs the product on
+// twiddles copied into LDS at entry (no L2 / HBM latency inside the transforms) and writes c back
+// in system-scope write-through stores (the host takes the request as done when every word of c
+// has changed from the pending marker).  The request half of the mailbox (req) is device memory
+// the host writes through its BAR mapping, so polls and operand loads stay on the device; c goes
+// to host memory (launch.hpp ServerReq / ServerBox).  n = 256, one product: the two-wave path
+// above.  Otherwise one wave runs the fused product of k_rows (64 / (n / 16) products per wave,
+// exchanges ordered per wave; a single product of n = 512 transforms a and b on two lane groups,
+// b's result handed to a's lanes by lane permutes).  It leaves on stop, after idle_ticks without
+// a request or after life_ticks in all (the host relaunches it on demand), so every wave always
+// ends -- the FPGA's GO / done-all handshake without a kernel launch per call.
 template <class A, int LOGS>
-__global__ __launch_bounds__(64) void k_server(KParams<A> P, const ServerReq *req, ServerBox *box,
-                                               unsigned tw_pairs, unsigned long long idle_ticks,
-                                               unsigned long long life_ticks) {
+__global__ __launch_bounds__(LOGS == 8 ? 128 : 64) void k_server(
+    KParams<A> P, const ServerReq *req, ServerBox *box, unsigned tw_pairs,
+    unsigned long long idle_ticks, unsigned long long life_ticks) {
   using W = typename A::word;
   using Gr = Groups<LOGS, kWT<A, LOGS>()>;
   constexpr int N = Gr::N, TP = N / 16, PB = 64 / TP, G = Gr::G, NP = Gr::NP;
   static_assert(sizeof(W) == 4 && TP <= 64, "u32 words, n <= 1024");
-  constexpr int KW = ServerBox::kWords;
+  constexpr bool kWide = LOGS == 8 && IsPlantard<A>::value && NTTMUL_BASE_D && A::kBaseD == 2;
+  constexpr int KW = ServerBox::kWords, NT = LOGS == 8 ? 128 : 64;
   __shared__ W lds[PB][NP];
   __shared__ uint4 stg[2][KW / 4];  // a, b as loaded (c as stored reuses stg[0])
-  __shared__ TwPair<W> twf[2 * N], twi[2 * N];  // launch_server: tw_pairs <= 2n
-  const int lane = threadIdx.x, pb = lane / TP, j = lane % TP;
-  for (unsigned i = lane; i < tw_pairs; i += 64) {
-    twf[i] = P.fw[i];
+  __shared__ TwPair<W> twf[N], twi[N];  // launch_server: tw_pairs <= n
+  __shared__ TwPair<W> wfu[kWide ? N : 1], wfs[kWide ? N : 1];
+  __shared__ unsigned s_go, s_quit;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, pb = lane / TP, j = lane % TP;
+  for (unsigned i = threadIdx.x; i < tw_pairs; i += NT) {
+    const TwPair<W> f = P.fw[i];
+    twf[i] = f;
     twi[i] = P.iw[i];
+    if constexpr (kWide) {  // the planner's per-entry form (arith_select.hpp p_signed_fw_entry)
+      const W sg = f.w >> 31;
+      const bool s = p_signed_fw_entry(LOGS, i);
+      wfu[i] = {f.w, s ? f.ws - sg : f.ws};
+      wfs[i] = {f.w, s ? f.ws : f.ws + sg};
+    }
   }
   P.fw = twf;
   P.iw = twi;
@@ -942,7 +1057,7 @@ __global__ __launch_bounds__(64) void k_server(KParams<A> P, const ServerReq *re
   constexpr int D = NTTMUL_BASE_D ? A::kBaseD : 0;
   unsigned seen = __hip_atomic_load(&box->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   seen = __builtin_amdgcn_readfirstlane(seen);
-  xsync<1>();  // the twiddles in LDS before the first transform
+  __syncthreads();  // the twiddles in LDS before the first transform
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   unsigned long long last = t0;
   // one poll at a time, NTTMUL_SERVER_POLL_SLEEP apart.  (Rounds 4b-4f kept three polls in
@@ -953,13 +1068,21 @@ __global__ __launch_bounds__(64) void k_server(KParams<A> P, const ServerReq *re
   for (;;) {
     unsigned go = seen;
     bool quit = false;
-    for (;;) {
-      go = __builtin_amdgcn_readfirstlane(
-          __hip_atomic_load(&req->go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-      if (go != seen) break;
-      const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-      if ((quit = now - last > idle_ticks || now - t0 > life_ticks)) break;
-      __builtin_amdgcn_s_sleep(kSleep);
+    if (wave == 0) {
+      for (;;) {
+        go = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(&req->go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+        if (go != seen) break;
+        const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+        if ((quit = now - last > idle_ticks || now - t0 > life_ticks)) break;
+        __builtin_amdgcn_s_sleep(kSleep);
+      }
+    }
+    if constexpr (NT > 64) {  // the other wave waits at the barrier while wave 0 polls
+      if (threadIdx.x == 0) s_go = go, s_quit = quit;
+      __syncthreads();
+      go = __builtin_amdgcn_readfirstlane(s_go);
+      quit = __builtin_amdgcn_readfirstlane(s_quit) != 0;
     }
     if (quit) break;
     const unsigned long long now = __builtin_amdgcn_s_memrealtime();
@@ -971,51 +1094,97 @@ __global__ __launch_bounds__(64) void k_server(KParams<A> P, const ServerReq *re
     st[0] = __builtin_amdgcn_s_memrealtime();
 #endif
     const int q4 = count * (N / 4);  // 16-byte quads per operand (count <= PB, so <= KW / 4)
-    {  // system-scope (sc0 sc1) loads: the host's writes reach memory behind any cached copy
-      const auto ra = span_rsrc(req->a, KW), rb = span_rsrc(req->b, KW);
-      for (int i = lane; i < q4; i += 64) {
-        const auto va = __builtin_amdgcn_raw_buffer_load_b128(ra, i * 16, 0, 17);
-        const auto vb = __builtin_amdgcn_raw_buffer_load_b128(rb, i * 16, 0, 17);
-        stg[0][i] = make_uint4(va[0], va[1], va[2], va[3]);
-        stg[1][i] = make_uint4(vb[0], vb[1], vb[2], vb[3]);
-      }
-    }
-    xsync<1>();
-    const W *sa = (const W *)stg[0], *sb = (const W *)stg[1];
-    // one product of n <= 512: lane group 0 transforms a, group 1 b (then hands b over)
-    const bool split = PB >= 2 && count == 1;
-    const bool live = pb < count;
-    W x[16], y[16];
-    {
-      const int base = (live ? pb : 0) * N + Gr::base(0, j);
-      const W *src = split && pb == 1 ? sb : sa;
+    if (kWide && count == 1) {
+      if constexpr (kWide) {
+        // wave w loads operand w in layout 6 (system scope: the host's writes reach memory
+        // behind any cached copy) and transforms it
+        uint32_t x[4];
+        const auto ro = span_rsrc(wave ? req->b : req->a, KW);
 #pragma unroll
-      for (int k = 0; k < 16; k++) {
-        x[k] = src[base + Gr::off(0, k)];
-        y[k] = sb[base + Gr::off(0, k)];
-      }
-    }
-    TwPair<W> zw[16];
+        for (int i = 0; i < 4; i++)
+          x[i] = __builtin_amdgcn_raw_buffer_load_b32(ro, (lane + 64 * i) * 4, 0, 17);
 #ifdef NTTMUL_CLOCK_STAMPS
-    st[1] = __builtin_amdgcn_s_memrealtime();
-    st[4] = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_s_waitcnt(0);
+        st[1] = __builtin_amdgcn_s_memrealtime();
+        st[4] = __builtin_amdgcn_s_memtime();
 #endif
-    if (split) {
-      fwd_all<A, LOGS, 0, 1, D, 1>(P.ar, x, y, lx, lx, P.fw, j, 0, 0, zw);
+        uint32_t *lw = lds[wave];
+        wide_fwd(P.ar, x, wfu, wfs, lw, lane);
+        // both transforms to the block layout (one 4-coefficient base block per lane of wave 0)
 #pragma unroll
-      for (int k = 0; k < 16; k++)  // group 1's transformed b to group 0's lanes, same j
-        y[k] = (W)__builtin_amdgcn_ds_bpermute((lane + TP) << 2, (int)x[k]);
-    } else {
-      fwd_all<A, LOGS, 0, 2, D, 1>(P.ar, x, y, lx, lx, P.fw, j, 0, 0, zw);
-    }
-    base_mult<A, LOGS, D>(P.ar, x, y, zw, j);
-    inv_all<A, LOGS, G - 1, true, D, 1>(P, x, y, lx, lx, P.iw, j, 0, 0);
+        for (int i = 0; i < 4; i++) lw[wl_pad(wl_elem<2>(lane, i))] = x[i];
+        __syncthreads();
+        if (wave == 0) {
+          uint32_t y[4];
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            x[i] = lds[0][wl_pad(wl_elem<0>(lane, i))];
+            y[i] = lds[1][wl_pad(wl_elem<0>(lane, i))];
+          }
+          xsync<1>();
+          // block lane: elements 4 lane .. 4 lane + 3, a residue mod x^4 -+ w with w the stage-5
+          // entry 32 + lane / 2, minus for odd lanes (the stage's differences)
+          const TwPair<uint32_t> z = wfs[32 + (lane >> 1)];
+          P.ar.basemul4_lane(x, y, z.w, z.ws, lane & 1);
+          wl_exchange<0, 2>(x, lds[0], lane);
+          wide_inv(P, x, twi, lds[0], lane);
 #ifdef NTTMUL_CLOCK_STAMPS
-    __builtin_amdgcn_sched_barrier(0);
-    st[2] = __builtin_amdgcn_s_memrealtime();
-    st[5] = __builtin_amdgcn_s_memtime();
+          __builtin_amdgcn_sched_barrier(0);
+          st[2] = __builtin_amdgcn_s_memrealtime();
+          st[5] = __builtin_amdgcn_s_memtime();
 #endif
-    {
+          // (the host watches c itself, see below: system-scope write-through stores)
+          const auto rc = span_rsrc(box->c, KW);
+#pragma unroll
+          for (int i = 0; i < 4; i++)
+            __builtin_amdgcn_raw_buffer_store_b32(x[i], rc, (lane + 64 * i) * 4, 0, 17);
+        }
+      }
+    } else if (wave == 0) {
+      {  // system-scope (sc0 sc1) loads: the host's writes reach memory behind any cached copy
+        const auto ra = span_rsrc(req->a, KW), rb = span_rsrc(req->b, KW);
+        for (int i = lane; i < q4; i += 64) {
+          const auto va = __builtin_amdgcn_raw_buffer_load_b128(ra, i * 16, 0, 17);
+          const auto vb = __builtin_amdgcn_raw_buffer_load_b128(rb, i * 16, 0, 17);
+          stg[0][i] = make_uint4(va[0], va[1], va[2], va[3]);
+          stg[1][i] = make_uint4(vb[0], vb[1], vb[2], vb[3]);
+        }
+      }
+      xsync<1>();
+      const W *sa = (const W *)stg[0], *sb = (const W *)stg[1];
+      // one product of n <= 512: lane group 0 transforms a, group 1 b (then hands b over)
+      const bool split = PB >= 2 && count == 1;
+      const bool live = pb < count;
+      W x[16], y[16];
+      {
+        const int base = (live ? pb : 0) * N + Gr::base(0, j);
+        const W *src = split && pb == 1 ? sb : sa;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+          x[k] = src[base + Gr::off(0, k)];
+          y[k] = sb[base + Gr::off(0, k)];
+        }
+      }
+      TwPair<W> zw[16];
+#ifdef NTTMUL_CLOCK_STAMPS
+      st[1] = __builtin_amdgcn_s_memrealtime();
+      st[4] = __builtin_amdgcn_s_memtime();
+#endif
+      if (split) {
+        fwd_all<A, LOGS, 0, 1, D, 1>(P.ar, x, y, lx, lx, P.fw, j, 0, 0, zw);
+#pragma unroll
+        for (int k = 0; k < 16; k++)  // group 1's transformed b to group 0's lanes, same j
+          y[k] = (W)__builtin_amdgcn_ds_bpermute((lane + TP) << 2, (int)x[k]);
+      } else {
+        fwd_all<A, LOGS, 0, 2, D, 1>(P.ar, x, y, lx, lx, P.fw, j, 0, 0, zw);
+      }
+      base_mult<A, LOGS, D>(P.ar, x, y, zw, j);
+      inv_all<A, LOGS, G - 1, true, D, 1>(P, x, y, lx, lx, P.iw, j, 0, 0);
+#ifdef NTTMUL_CLOCK_STAMPS
+      __builtin_amdgcn_sched_barrier(0);
+      st[2] = __builtin_amdgcn_s_memrealtime();
+      st[5] = __builtin_amdgcn_s_memtime();
+#endif
       W *sc = (W *)stg[0];
       if (live) {
         const int base = pb * N + Gr::base(0, j);
@@ -1039,18 +1208,21 @@ __global__ __launch_bounds__(64) void k_server(KParams<A> P, const ServerReq *re
       }
     }
 #ifdef NTTMUL_CLOCK_STAMPS  // diagnostic build: c landed (fence), then the stamps, then done
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    st[3] = __builtin_amdgcn_s_memrealtime();
-    if (threadIdx.x == 0)  // vector stores from lane 0, released with done below
-      for (int k = 0; k < 6; k++) box->stamp[k] = st[k];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(&box->done, go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (wave == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      st[3] = __builtin_amdgcn_s_memrealtime();
+      if (threadIdx.x == 0)  // vector stores from lane 0, released with done below
+        for (int k = 0; k < 6; k++) box->stamp[k] = st[k];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(&box->done, go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 #endif
     seen = go;
     last = now;
-    xsync<1>();  // the next request's loads land in stg after every lane has stored c
+    // the next request's loads land in stg / lds after every lane has stored c
+    if constexpr (NT > 64) __syncthreads(); else xsync<1>();
   }
 }
 
@@ -1974,12 +2146,12 @@ hipError_t launch_server(const LaunchTables &T, const ServerReq *req, ServerBox 
                          hipStream_t s) {
   const size_t pairs = T.tw_bytes / sizeof(TwPair<uint32_t>);
   if (T.word_bits != 32 || a32_kind(T.q) != A32Kind::Plantard || T.logn < 8 || T.logn > 10 ||
-      pairs > (2u << T.logn))
+      pairs > (1u << T.logn))
     return hipErrorNotSupported;
   const KParams<Arith32P> P = product_params<Arith32P>(T);
   const unsigned tp = (unsigned)pairs;
   switch (T.logn) {
-    case 8: hipLaunchKernelGGL((k_server<Arith32P, 8>), dim3(1), dim3(64), 0, s, P, req, box, tp, idle_ticks, life_ticks); break;
+    case 8: hipLaunchKernelGGL((k_server<Arith32P, 8>), dim3(1), dim3(128), 0, s, P, req, box, tp, idle_ticks, life_ticks); break;
     case 9: hipLaunchKernelGGL((k_server<Arith32P, 9>), dim3(1), dim3(64), 0, s, P, req, box, tp, idle_ticks, life_ticks); break;
     default: hipLaunchKernelGGL((k_server<Arith32P, 10>), dim3(1), dim3(64), 0, s, P, req, box, tp, idle_ticks, life_ticks); break;
   }

@@ -20,7 +20,7 @@ struct LaunchTables {
   uint64_t r2;             // R^2 mod q (standalone pointwise product)
   const void *fw, *iw;     // forward / inverse twiddle (value, companion) pairs, n entries
                            // (planner.cpp tw_pair: Shoup, or Montgomery form for Arith32)
-  size_t tw_bytes = 0;     // bytes of each of fw, iw (the typed Plantard forward table holds 2n)
+  size_t tw_bytes = 0;     // bytes of each of fw, iw (2n pairs with Arith32's centred copies)
   int cus;                 // compute units of the device (launch-shape thresholds)
   int prio = 0;            // nttmul_params.issue_prio: -1 never, 0 automatic, 1 always
   int prio_ok = 1;         // 0: the previous product launch of this context went to another
@@ -64,7 +64,7 @@ hipError_t launch_bitrev(const void *in, void *out, uint32_t logn, size_t batch,
 hipError_t launch_fill(void *a, void *b, uint32_t logn, uint64_t q, uint64_t seed, uint64_t p0,
                        size_t count, int io_bits, hipStream_t s);
 // Mailbox of the small-transaction device server (k_server, nttmul.cpp Server), shared by one
-// host caller and one resident single-wave kernel -- the MI355X form of the FPGA communicator's
+// host caller and one resident kernel -- the MI355X form of the FPGA communicator's
 // mode-3 GO + WaitForDoneAll polling (NTT_PCIECommunicationv2.c:83-107, 211-215).  The host sets
 // c to kPending, writes a and b, then the go word (seq << 8) | count; the kernel (polling go)
 // multiplies and writes c, and the request is complete when no word of c is kPending.  One word
@@ -96,7 +96,7 @@ struct ServerReq {
 // Launch the server for products of n = 2^logn <= 1024 u32 words (q < 2^31) on stream s; it
 // leaves after idle_ticks of the 100 MHz clock without a request, after life_ticks in all, or
 // on a stop request.  hipErrorNotSupported for other (n, q) or twiddle tables larger than the
-// kernel's LDS copy (2n pairs each).
+// kernel's LDS copy (n pairs each).
 hipError_t launch_server(const LaunchTables &T, const ServerReq *req, ServerBox *box,
                          unsigned long long idle_ticks, unsigned long long life_ticks,
                          hipStream_t s);

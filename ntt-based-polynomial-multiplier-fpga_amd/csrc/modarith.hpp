@@ -462,6 +462,33 @@ struct Arith32P {
 #endif
     }
   }
+  // basemul<4, NEG, true> with NEG known per lane (kernels.hip server_wide256: one block per
+  // lane): a and b of a -w block arrive as signed differences, of a +w block as lazy sums; z is
+  // in signed form, which the signed-input product multiplies exactly for canonical inputs.
+  __device__ __forceinline__ void basemul4_lane(uint32_t (&a)[4], const uint32_t (&b)[4],
+                                                uint32_t z0, uint32_t z1s, bool neg) const {
+    uint32_t ar[4], br[4], bz[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      ar[i] = neg ? cadd(a[i]) : csub(a[i], q);
+      br[i] = neg ? cadd(b[i]) : csub(b[i], q);
+    }
+#pragma unroll
+    for (int i = 1; i < 4; i++) {
+      const uint32_t t = pmul_s(br[i], z0, z1s);
+      bz[i] = neg ? q - t : t;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      uint64_t s = 0;
+#pragma unroll
+      for (int i = 0; i < 4; i++) s += (uint64_t)ar[i] * (i <= k ? br[k - i] : bz[4 + k - i]);
+      // (the fold and reduction of basemul, NTTMUL_P_FOLD)
+      const uint64_t s2 = (uint64_t)(uint32_t)(s >> 32) * c32 + (uint32_t)s;
+      const uint32_t m = (uint32_t)s2 * qinv_neg;
+      a[k] = csub((uint32_t)((s2 + (uint64_t)m * q) >> 32), q);
+    }
+  }
 };
 
 // Arith32P with base blocks of 8 coefficients (D = 3): one butterfly stage fewer in each of the

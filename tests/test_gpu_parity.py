@@ -630,6 +630,29 @@ def test_small_server_products(n, batch, torch_cuda):
             assert launch.last_host_path() == 2
 
 
+@pytest.mark.parametrize("cyclic", [False, True])
+def test_small_server_two_wave_path(cyclic, torch_cuda):
+    """Single n = 256 products take the server's two-wave path (kernels.hip server wide path:
+    4 coefficients per lane, the planner's twiddles re-typed in LDS, the base multiplication's
+    sign chosen per lane): random primes of every Plantard width (2n | q - 1, 14..31 bits),
+    random and all-(q - 1) operands, negacyclic against the restated reference product and
+    cyclic (FPGA-compat) against the schoolbook product."""
+    n = 256
+    for q in _random_primes([14, 17, 20, 24, 28, 30, 31], 9, seed=11 + cyclic) + [Q0, Q31, Q31HI]:
+        P = O.Plan(n, q)
+        ctx = _ctx(n, q, cyclic=cyclic)
+        for it in range(4):
+            a, b = O.fill_inputs(n, q, 7 * it + (q & 0xFF), 1)
+            if it == 1:
+                a[0] = q - 1
+            if it == 2:
+                a[0] = b[0] = q - 1
+            got = ctx.multiply(a.astype(np.uint32), b.astype(np.uint32)).astype(np.uint64)
+            assert ctx.last_host_path() == 3
+            exp = O.cyclic_schoolbook(a[0], b[0], n, q) if cyclic else P.product_merged(a[0], b[0])
+            assert np.array_equal(got[0], exp), (q, cyclic, it)
+
+
 def test_small_server_answers_promptly(torch_cuda):
     """A request is answered while the server kernel keeps running, not when it leaves: 200
     back-to-back n = 256 products through the server take well under the 20 ms idle exit each
