@@ -932,81 +932,78 @@ __device__ __forceinline__ void wl_exchange(uint32_t (&x)[4], uint32_t *lx, int 
   for (int i = 0; i < 4; i++) x[i] = lx[wl_pad(wl_elem<PT>(t, i))];
   xsync<1>();
 }
+// A lane's twiddle pairs for one request (the same every request: loaded into registers once,
+// so the transforms read no memory): forward f[0..8] in stage order, the base block's z, inverse
+// i[0..7] in stage order (5, 4, 3, 2, 1)
+struct WideTw {
+  TwPair<uint32_t> f[9], z, i[8];
+};
+__device__ __forceinline__ WideTw wide_tw(const TwPair<uint32_t> *fu, const TwPair<uint32_t> *fs,
+                                          const TwPair<uint32_t> *iw, int t) {
+  WideTw w;
+  const int k3 = 8 + ((t >> 4) << 1), k5 = 32 + ((t >> 2) << 1);
+  w.f[0] = fu[1];               // stage 0: entry 1
+  w.f[1] = fu[2];               // stage 1: entries 2 (sums) and 3 (differences)
+  w.f[2] = fs[3];
+  w.f[3] = fu[4 + (t >> 4)];    // stage 2: entry 4 + e >> 6 (layout 4)
+  w.f[4] = fu[k3];              // stage 3: entry 8 + e >> 5
+  w.f[5] = fs[k3 + 1];
+  w.f[6] = fu[16 + (t >> 2)];   // stage 4: entry 16 + e >> 4 (layout 2)
+  w.f[7] = fu[k5];              // stage 5: entry 32 + e >> 3
+  w.f[8] = fs[k5 + 1];
+  w.z = fs[32 + (t >> 1)];      // block lane t: elements 4t .. 4t + 3 (layout 0)
+  w.i[0] = iw[k5];
+  w.i[1] = iw[k5 + 1];
+  w.i[2] = iw[16 + (t >> 2)];
+  w.i[3] = iw[k3];
+  w.i[4] = iw[k3 + 1];
+  w.i[5] = iw[4 + (t >> 4)];
+  w.i[6] = iw[2];
+  w.i[7] = iw[3];
+  return w;
+}
 // forward CT, stages 0-5 of the incomplete transform (D = 2), X canonical on entry (the API
-// contract); leaves layout 2 (element bits 2, 3 in the registers)
-__device__ __forceinline__ void wide_fwd(const Arith32P &ar, uint32_t (&x)[4],
-                                         const TwPair<uint32_t> *fu, const TwPair<uint32_t> *fs,
+// contract); layout 6 in, layout 2 out (element bits 2, 3 in the registers)
+__device__ __forceinline__ void wide_fwd(const Arith32P &ar, uint32_t (&x)[4], const WideTw &w,
                                          uint32_t *lx, int t) {
-  {  // stage 0 (d 128: register bit 1), entry 1
-    const TwPair<uint32_t> w = fu[1];
-    ar.template ct<true, false, true>(x[0], x[2], w.w, w.ws);
-    ar.template ct<true, false, true>(x[1], x[3], w.w, w.ws);
-  }
-  {  // stage 1 (d 64: register bit 0), entries 2 (sums) and 3 (differences)
-    const TwPair<uint32_t> w0 = fu[2], w1 = fs[3];
-    ar.template ct<false, false, false>(x[0], x[1], w0.w, w0.ws);
-    ar.template ct<false, true, false>(x[2], x[3], w1.w, w1.ws);
-  }
+  // stage 0 (d 128: register bit 1)
+  ar.template ct<true, false, true>(x[0], x[2], w.f[0].w, w.f[0].ws);
+  ar.template ct<true, false, true>(x[1], x[3], w.f[0].w, w.f[0].ws);
+  // stage 1 (d 64: register bit 0), the second pair on stage 0's differences
+  ar.template ct<false, false, false>(x[0], x[1], w.f[1].w, w.f[1].ws);
+  ar.template ct<false, true, false>(x[2], x[3], w.f[2].w, w.f[2].ws);
   wl_exchange<6, 4>(x, lx, t);
-  {  // stage 2 (d 32: register bit 1), entry 4 + e >> 6
-    const TwPair<uint32_t> w = fu[4 + (t >> 4)];
-    ar.template ct<false, false, true>(x[0], x[2], w.w, w.ws);
-    ar.template ct<false, false, true>(x[1], x[3], w.w, w.ws);
-  }
-  {  // stage 3 (d 16: register bit 0), entry 8 + e >> 5
-    const int k = 8 + ((t >> 4) << 1);
-    const TwPair<uint32_t> w0 = fu[k], w1 = fs[k + 1];
-    ar.template ct<false, false, false>(x[0], x[1], w0.w, w0.ws);
-    ar.template ct<false, true, false>(x[2], x[3], w1.w, w1.ws);
-  }
+  // stage 2 (d 32: register bit 1)
+  ar.template ct<false, false, true>(x[0], x[2], w.f[3].w, w.f[3].ws);
+  ar.template ct<false, false, true>(x[1], x[3], w.f[3].w, w.f[3].ws);
+  // stage 3 (d 16: register bit 0)
+  ar.template ct<false, false, false>(x[0], x[1], w.f[4].w, w.f[4].ws);
+  ar.template ct<false, true, false>(x[2], x[3], w.f[5].w, w.f[5].ws);
   wl_exchange<4, 2>(x, lx, t);
-  {  // stage 4 (d 8: register bit 1), entry 16 + e >> 4
-    const TwPair<uint32_t> w = fu[16 + (t >> 2)];
-    ar.template ct<false, false, true>(x[0], x[2], w.w, w.ws);
-    ar.template ct<false, false, true>(x[1], x[3], w.w, w.ws);
-  }
-  {  // stage 5 (d 4: register bit 0), entry 32 + e >> 3; differences stay signed
-    const int k = 32 + ((t >> 2) << 1);
-    const TwPair<uint32_t> w0 = fu[k], w1 = fs[k + 1];
-    ar.template ct<false, false, true>(x[0], x[1], w0.w, w0.ws);
-    ar.template ct<false, true, true>(x[2], x[3], w1.w, w1.ws);
-  }
+  // stage 4 (d 8: register bit 1)
+  ar.template ct<false, false, true>(x[0], x[2], w.f[6].w, w.f[6].ws);
+  ar.template ct<false, false, true>(x[1], x[3], w.f[6].w, w.f[6].ws);
+  // stage 5 (d 4: register bit 0); the differences stay signed for the base multiplication
+  ar.template ct<false, false, true>(x[0], x[1], w.f[7].w, w.f[7].ws);
+  ar.template ct<false, true, true>(x[2], x[3], w.f[8].w, w.f[8].ws);
 }
 // inverse GS from layout 2 (the first D = 2 stages are the base multiplication's), F folded into
 // stage 0; leaves layout 6 (e = t + 64 i), canonical
 __device__ __forceinline__ void wide_inv(const KParams<Arith32P> &P, uint32_t (&x)[4],
-                                         const TwPair<uint32_t> *iw, uint32_t *lx, int t) {
-  {  // stage 5 (register bit 0), entry 32 + e >> 3
-    const int k = 32 + ((t >> 2) << 1);
-    const TwPair<uint32_t> w0 = iw[k], w1 = iw[k + 1];
-    P.ar.gs(x[0], x[1], w0.w, w0.ws);
-    P.ar.gs(x[2], x[3], w1.w, w1.ws);
-  }
-  {  // stage 4 (register bit 1), entry 16 + e >> 4
-    const TwPair<uint32_t> w = iw[16 + (t >> 2)];
-    P.ar.gs(x[0], x[2], w.w, w.ws);
-    P.ar.gs(x[1], x[3], w.w, w.ws);
-  }
+                                         const WideTw &w, uint32_t *lx, int t) {
+  P.ar.gs(x[0], x[1], w.i[0].w, w.i[0].ws);  // stage 5 (register bit 0)
+  P.ar.gs(x[2], x[3], w.i[1].w, w.i[1].ws);
+  P.ar.gs(x[0], x[2], w.i[2].w, w.i[2].ws);  // stage 4 (register bit 1)
+  P.ar.gs(x[1], x[3], w.i[2].w, w.i[2].ws);
   wl_exchange<2, 4>(x, lx, t);
-  {  // stage 3 (register bit 0), entry 8 + e >> 5
-    const int k = 8 + ((t >> 4) << 1);
-    const TwPair<uint32_t> w0 = iw[k], w1 = iw[k + 1];
-    P.ar.gs(x[0], x[1], w0.w, w0.ws);
-    P.ar.gs(x[2], x[3], w1.w, w1.ws);
-  }
-  {  // stage 2 (register bit 1), entry 4 + e >> 6
-    const TwPair<uint32_t> w = iw[4 + (t >> 4)];
-    P.ar.gs(x[0], x[2], w.w, w.ws);
-    P.ar.gs(x[1], x[3], w.w, w.ws);
-  }
+  P.ar.gs(x[0], x[1], w.i[3].w, w.i[3].ws);  // stage 3
+  P.ar.gs(x[2], x[3], w.i[4].w, w.i[4].ws);
+  P.ar.gs(x[0], x[2], w.i[5].w, w.i[5].ws);  // stage 2
+  P.ar.gs(x[1], x[3], w.i[5].w, w.i[5].ws);
   wl_exchange<4, 6>(x, lx, t);
-  {  // stage 1 (register bit 0), entries 2 and 3
-    const TwPair<uint32_t> w0 = iw[2], w1 = iw[3];
-    P.ar.gs(x[0], x[1], w0.w, w0.ws);
-    P.ar.gs(x[2], x[3], w1.w, w1.ws);
-  }
-  // stage 0 (register bit 1) with F
-  P.ar.gs_scaled(x[0], x[2], P.f, P.fs, P.wf, P.wfs);
+  P.ar.gs(x[0], x[1], w.i[6].w, w.i[6].ws);  // stage 1
+  P.ar.gs(x[2], x[3], w.i[7].w, w.i[7].ws);
+  P.ar.gs_scaled(x[0], x[2], P.f, P.fs, P.wf, P.wfs);  // stage 0 with F
   P.ar.gs_scaled(x[1], x[3], P.f, P.fs, P.wf, P.wfs);
 }
 
@@ -1058,6 +1055,8 @@ __global__ __launch_bounds__(LOGS == 8 ? 128 : 64) void k_server(
   unsigned seen = __hip_atomic_load(&box->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   seen = __builtin_amdgcn_readfirstlane(seen);
   __syncthreads();  // the twiddles in LDS before the first transform
+  WideTw wtw;
+  if constexpr (kWide) wtw = wide_tw(wfu, wfs, twi, lane);
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   unsigned long long last = t0;
   // one poll at a time, NTTMUL_SERVER_POLL_SLEEP apart.  (Rounds 4b-4f kept three polls in
@@ -1109,7 +1108,7 @@ __global__ __launch_bounds__(LOGS == 8 ? 128 : 64) void k_server(
         st[4] = __builtin_amdgcn_s_memtime();
 #endif
         uint32_t *lw = lds[wave];
-        wide_fwd(P.ar, x, wfu, wfs, lw, lane);
+        wide_fwd(P.ar, x, wtw, lw, lane);
         // both transforms to the block layout (one 4-coefficient base block per lane of wave 0)
 #pragma unroll
         for (int i = 0; i < 4; i++) lw[wl_pad(wl_elem<2>(lane, i))] = x[i];
@@ -1124,10 +1123,9 @@ __global__ __launch_bounds__(LOGS == 8 ? 128 : 64) void k_server(
           xsync<1>();
           // block lane: elements 4 lane .. 4 lane + 3, a residue mod x^4 -+ w with w the stage-5
           // entry 32 + lane / 2, minus for odd lanes (the stage's differences)
-          const TwPair<uint32_t> z = wfs[32 + (lane >> 1)];
-          P.ar.basemul4_lane(x, y, z.w, z.ws, lane & 1);
+          P.ar.basemul4_lane(x, y, wtw.z.w, wtw.z.ws, lane & 1);
           wl_exchange<0, 2>(x, lds[0], lane);
-          wide_inv(P, x, twi, lds[0], lane);
+          wide_inv(P, x, wtw, lds[0], lane);
 #ifdef NTTMUL_CLOCK_STAMPS
           __builtin_amdgcn_sched_barrier(0);
           st[2] = __builtin_amdgcn_s_memrealtime();
