@@ -962,6 +962,35 @@ __device__ __forceinline__ WideTw wide_tw(const TwPair<uint32_t> *fu, const TwPa
   w.i[7] = iw[3];
   return w;
 }
+// Layout changes inside the wave without LDS.  Layouts 6 and 4 differ by swapping register bit 0
+// with lane bit 4 and register bit 1 with lane bit 5: one v_permlane16_swap / v_permlane32_swap
+// per register pair.  Layouts 4 and 2 differ by register bits 0, 1 against lane bits 2, 3: two
+// DPP row shifts (by 4 or 8 lanes within a 16-lane row) and two selects per register pair.  Both
+// are involutions, so the inverse uses them back.
+__device__ __forceinline__ void wl_swap_64(uint32_t (&x)[4]) {
+  auto s0 = __builtin_amdgcn_permlane16_swap(x[0], x[1], false, false);
+  auto s1 = __builtin_amdgcn_permlane16_swap(x[2], x[3], false, false);
+  x[0] = s0[0], x[1] = s0[1], x[2] = s1[0], x[3] = s1[1];
+  auto s2 = __builtin_amdgcn_permlane32_swap(x[0], x[2], false, false);
+  auto s3 = __builtin_amdgcn_permlane32_swap(x[1], x[3], false, false);
+  x[0] = s2[0], x[2] = s2[1], x[1] = s3[0], x[3] = s3[1];
+}
+// register bit r <-> lane bit log2(SH) for the pair (x[A], x[A + 1 << r]): lanes with that bit
+// set take the partner register's value from SH lanes below, the others from SH lanes above
+template <int SH, int A, int B>
+__device__ __forceinline__ void wl_swap_dpp(uint32_t (&x)[4], int t) {
+  const uint32_t up = __builtin_amdgcn_update_dpp(0u, x[B], 0x110 + SH, 0xF, 0xF, false);  // row_shr
+  const uint32_t dn = __builtin_amdgcn_update_dpp(0u, x[A], 0x100 + SH, 0xF, 0xF, false);  // row_shl
+  const bool hi = (t & SH) != 0;
+  x[A] = hi ? up : x[A];
+  x[B] = hi ? x[B] : dn;
+}
+__device__ __forceinline__ void wl_swap_42(uint32_t (&x)[4], int t) {
+  wl_swap_dpp<4, 0, 1>(x, t);
+  wl_swap_dpp<4, 2, 3>(x, t);
+  wl_swap_dpp<8, 0, 2>(x, t);
+  wl_swap_dpp<8, 1, 3>(x, t);
+}
 // forward CT, stages 0-5 of the incomplete transform (D = 2), X canonical on entry (the API
 // contract); layout 6 in, layout 2 out (element bits 2, 3 in the registers)
 __device__ __forceinline__ void wide_fwd(const Arith32P &ar, uint32_t (&x)[4], const WideTw &w,
@@ -972,14 +1001,14 @@ __device__ __forceinline__ void wide_fwd(const Arith32P &ar, uint32_t (&x)[4], c
   // stage 1 (d 64: register bit 0), the second pair on stage 0's differences
   ar.template ct<false, false, false>(x[0], x[1], w.f[1].w, w.f[1].ws);
   ar.template ct<false, true, false>(x[2], x[3], w.f[2].w, w.f[2].ws);
-  wl_exchange<6, 4>(x, lx, t);
+  wl_swap_64(x);
   // stage 2 (d 32: register bit 1)
   ar.template ct<false, false, true>(x[0], x[2], w.f[3].w, w.f[3].ws);
   ar.template ct<false, false, true>(x[1], x[3], w.f[3].w, w.f[3].ws);
   // stage 3 (d 16: register bit 0)
   ar.template ct<false, false, false>(x[0], x[1], w.f[4].w, w.f[4].ws);
   ar.template ct<false, true, false>(x[2], x[3], w.f[5].w, w.f[5].ws);
-  wl_exchange<4, 2>(x, lx, t);
+  wl_swap_42(x, t);
   // stage 4 (d 8: register bit 1)
   ar.template ct<false, false, true>(x[0], x[2], w.f[6].w, w.f[6].ws);
   ar.template ct<false, false, true>(x[1], x[3], w.f[6].w, w.f[6].ws);
@@ -995,12 +1024,12 @@ __device__ __forceinline__ void wide_inv(const KParams<Arith32P> &P, uint32_t (&
   P.ar.gs(x[2], x[3], w.i[1].w, w.i[1].ws);
   P.ar.gs(x[0], x[2], w.i[2].w, w.i[2].ws);  // stage 4 (register bit 1)
   P.ar.gs(x[1], x[3], w.i[2].w, w.i[2].ws);
-  wl_exchange<2, 4>(x, lx, t);
+  wl_swap_42(x, t);
   P.ar.gs(x[0], x[1], w.i[3].w, w.i[3].ws);  // stage 3
   P.ar.gs(x[2], x[3], w.i[4].w, w.i[4].ws);
   P.ar.gs(x[0], x[2], w.i[5].w, w.i[5].ws);  // stage 2
   P.ar.gs(x[1], x[3], w.i[5].w, w.i[5].ws);
-  wl_exchange<4, 6>(x, lx, t);
+  wl_swap_64(x);
   P.ar.gs(x[0], x[1], w.i[6].w, w.i[6].ws);  // stage 1
   P.ar.gs(x[2], x[3], w.i[7].w, w.i[7].ws);
   P.ar.gs_scaled(x[0], x[2], P.f, P.fs, P.wf, P.wfs);  // stage 0 with F
