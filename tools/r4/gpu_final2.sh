@@ -16,3 +16,7 @@ for i in 1 2 3; do
 done
 timeout -k 10 120 python tools/r4/server_latency.py > $OUT/server_latency.json 2> $OUT/server_latency.err || { tail -20 $OUT/server_latency.err; exit 1; }
 grep -A8 timeline $OUT/server_latency.json
+# the reference's own ntt256_product4 etc. on one core of this box (oracle/_ref, checked against
+# the oracle), beside the server's per-call time above
+timeout -k 10 120 python -c "import json, sys; sys.path.insert(0, '.'); from oracle import oracle as O; print(json.dumps({k: v * 1e6 for k, v in O.ref_anchors().items()}, indent=1))" > $OUT/ref_anchors_us.json || exit 1
+cat $OUT/ref_anchors_us.json
