@@ -1091,7 +1091,7 @@ __global__ __launch_bounds__(LOGS == 8 ? 128 : 64) void k_server(
   // one poll at a time, NTTMUL_SERVER_POLL_SLEEP apart.  (Rounds 4b-4f kept three polls in
   // flight 16 x 64 cycles apart, sized for reads across PCIe; with the request in device memory a
   // single poll is 1 us faster per request, and with it in host memory too:
-  // tools/microbench/mailbox_latency.hip, profiles/r4/r4g/mailbox_latency.json)
+  // tools/microbench/mailbox_latency.hip, profiles/r4/mailbox/)
   constexpr int kSleep = NTTMUL_SERVER_POLL_SLEEP;
   for (;;) {
     unsigned go = seen;

@@ -44,7 +44,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *p, unsigned b
 }
 
 // one wave: poll go, load a and b (words per request), c = a ^ b to host memory
-template <bool STAGGER>
+template <int MODE, bool FENCE = true>
 __global__ __launch_bounds__(64) void k_serve(Req *rq, Resp *rs, int words, unsigned spin,
                                               unsigned long long idle, unsigned long long life) {
   __shared__ uint4 sa[kWords / 4], sb[kWords / 4];
@@ -64,25 +64,34 @@ __global__ __launch_bounds__(64) void k_serve(Req *rq, Resp *rs, int words, unsi
       const unsigned long long now = __builtin_amdgcn_s_memrealtime();
       return now - last > idle || now - t0 > life;
     };
-    if constexpr (STAGGER) {  // the library server's loop: three polls in flight, s_sleep 16 apart
+    if constexpr (MODE >= 1) {  // several polls in flight: 3, s_sleep 16 apart (MODE 1) or 4, s_sleep 1 apart (MODE 2)
+      constexpr int SL = MODE == 1 ? 16 : 1;
       unsigned p0 = poll();
-      __builtin_amdgcn_s_sleep(16);
+      __builtin_amdgcn_s_sleep(SL);
       unsigned p1 = poll();
-      __builtin_amdgcn_s_sleep(16);
+      __builtin_amdgcn_s_sleep(SL);
+      unsigned p2 = MODE == 2 ? poll() : 0u;
+      if (MODE == 2) __builtin_amdgcn_s_sleep(SL);
       bool quit = false;
       for (;;) {
-        unsigned p2 = poll();
+        unsigned p3 = poll();
         if ((go = __builtin_amdgcn_readfirstlane(p0)) != seen) break;
         if ((quit = gone())) break;
-        __builtin_amdgcn_s_sleep(16);
+        __builtin_amdgcn_s_sleep(SL);
         p0 = poll();
         if ((go = __builtin_amdgcn_readfirstlane(p1)) != seen) break;
         if ((quit = gone())) break;
-        __builtin_amdgcn_s_sleep(16);
+        __builtin_amdgcn_s_sleep(SL);
         p1 = poll();
-        if ((go = __builtin_amdgcn_readfirstlane(p2)) != seen) break;
+        if (MODE == 2) {
+          if ((go = __builtin_amdgcn_readfirstlane(p2)) != seen) break;
+          if ((quit = gone())) break;
+          __builtin_amdgcn_s_sleep(SL);
+          p2 = poll();
+        }
+        if ((go = __builtin_amdgcn_readfirstlane(p3)) != seen) break;
         if ((quit = gone())) break;
-        __builtin_amdgcn_s_sleep(16);
+        __builtin_amdgcn_s_sleep(SL);
       }
       if (quit) return;
     } else {
@@ -94,7 +103,7 @@ __global__ __launch_bounds__(64) void k_serve(Req *rq, Resp *rs, int words, unsi
       }
     }
     if (go == 0xFFFFFFFFu) return;  // stop
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    if (FENCE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // (the loads below are sc0 sc1)
     const int q4 = words / 4;
     for (int i = lane; i < q4; i += 64) {  // system-scope (sc0 sc1) 16-byte loads
       auto va = __builtin_amdgcn_raw_buffer_load_b128(ra, i * 16, 0, 17);
@@ -118,6 +127,16 @@ __global__ __launch_bounds__(64) void k_serve(Req *rq, Resp *rs, int words, unsi
   }
 }
 
+// a chain of n dependent system-scope loads of go (the next address depends on the last value)
+__global__ void k_chain(Req *rq, unsigned long long *out, int n) {
+  unsigned v = 0;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (int i = 0; i < n; i++)
+    v = __hip_atomic_load(&rq->go + (v & 0x80000000u ? 1 : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) *out = (t1 - t0) + (v == 0x12345678u);
+}
+
 static double pct(std::vector<double> v, double p) {
   std::sort(v.begin(), v.end());
   return v[(size_t)(p * (v.size() - 1))];
@@ -126,15 +145,19 @@ static double pct(std::vector<double> v, double p) {
 // host side of one variant: rq is what the host writes through (host or mapped device pointer),
 // drq what the kernel sees
 static void run(const char *name, Req *rq, Req *drq, Resp *rs, Resp *drs, int words, int calls,
-                bool wc_fence, bool stagger = false, unsigned spin = 0) {
+                bool wc_fence, int stagger = 0, unsigned spin = 0, bool fence = true) {
   hipStream_t s;
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   rq->go = 0;
   _mm_sfence();
-  if (stagger)
-    hipLaunchKernelGGL(k_serve<true>, dim3(1), dim3(64), 0, s, drq, drs, words, spin, 2000000ull, 100000000ull);
+  if (!fence)
+    hipLaunchKernelGGL((k_serve<0, false>), dim3(1), dim3(64), 0, s, drq, drs, words, spin, 2000000ull, 100000000ull);
+  else if (stagger == 2)
+    hipLaunchKernelGGL(k_serve<2>, dim3(1), dim3(64), 0, s, drq, drs, words, spin, 2000000ull, 100000000ull);
+  else if (stagger == 1)
+    hipLaunchKernelGGL(k_serve<1>, dim3(1), dim3(64), 0, s, drq, drs, words, spin, 2000000ull, 100000000ull);
   else
-    hipLaunchKernelGGL(k_serve<false>, dim3(1), dim3(64), 0, s, drq, drs, words, spin, 2000000ull, 100000000ull);
+    hipLaunchKernelGGL(k_serve<0>, dim3(1), dim3(64), 0, s, drq, drs, words, spin, 2000000ull, 100000000ull);
   std::vector<unsigned> a(kWords), b(kWords);
   std::vector<double> us, us_w;
   unsigned seq = 0;
@@ -176,7 +199,7 @@ static void run(const char *name, Req *rq, Req *drq, Resp *rs, Resp *drs, int wo
   }
   printf("{\"variant\": \"%s\", \"poll\": \"%s\", \"spin_us\": %.2f, \"words\": %d, \"calls\": %d, "
          "\"bad_words\": %d, \"us_p10\": %.2f, \"us_p50\": %.2f, \"us_p90\": %.2f, \"host_write_us_p50\": %.2f}\n",
-         name, stagger ? "3 in flight, s_sleep 16" : "1, s_sleep 2", spin / 100.0, words, calls, bad,
+         name, !fence ? "1, s_sleep 2, no acquire fence" : stagger == 2 ? "4 in flight, s_sleep 1" : stagger ? "3 in flight, s_sleep 16" : "1, s_sleep 2", spin / 100.0, words, calls, bad,
          pct(us, 0.1), pct(us, 0.5), pct(us, 0.9), pct(us_w, 0.5));
 }
 
@@ -224,7 +247,10 @@ int main(int argc, char **argv) {
   CK(hipHostGetDevicePointer((void **)&dhq, hq, 0));
   memset(hq, 0, sizeof(Req));
   for (int w : {256, 512}) run("host_mailbox", hq, dhq, rs, drs, w, calls, false);
-  for (unsigned spin : {0u, 188u}) run("host_mailbox", hq, dhq, rs, drs, 256, calls, false, true, spin);
+  for (int rep = 0; rep < 2; rep++) {
+    run("host_mailbox", hq, dhq, rs, drs, 256, calls, false, 0, 0, true);
+    run("host_mailbox", hq, dhq, rs, drs, 256, calls, false, 0, 0, false);
+  }
 
   // V1: fine-grained device memory from HIP; the host's view from the pointer attributes / HSA
   Req *fq = nullptr;
@@ -272,8 +298,21 @@ int main(int argc, char **argv) {
     if (back != 12345) continue;
     for (int w : {256, 512}) run(v.name, v.host, v.dev, rs, drs, w, calls, true);
     if (v.dev != fq) continue;
-    for (bool st : {false, true})
-      for (unsigned spin : {0u, 188u}) run(v.name, v.host, v.dev, rs, drs, 256, calls, true, st, spin);
+    for (int rep = 0; rep < 3; rep++) {
+      run(v.name, v.host, v.dev, rs, drs, 256, calls, true, 0, 0, true);
+      run(v.name, v.host, v.dev, rs, drs, 256, calls, true, 0, 0, false);
+    }
+    for (int st : {2, 1}) run(v.name, v.host, v.dev, rs, drs, 256, calls, true, st, 0);
+    // latency of one system-scope load of the device-memory go word: a dependent chain
+    {
+      unsigned long long *d_t;
+      CK(hipMalloc(&d_t, 8));
+      hipLaunchKernelGGL(k_chain, dim3(1), dim3(64), 0, 0, v.dev, d_t, 256);
+      unsigned long long tk = 0;
+      CK(hipMemcpy(&tk, d_t, 8, hipMemcpyDeviceToHost));
+      printf("{\"variant\": \"%s\", \"poll_load_latency_ns\": %.1f}\n", v.name, tk * 10.0 / 256);
+      CK(hipFree(d_t));
+    }
   }
   return 0;
 }
