@@ -75,10 +75,12 @@ typedef struct {
   uint32_t scratch_mb;  /* n > 4096 products and reordered transforms: at most this many MiB per
                            scratch buffer; larger batches run in sub-batches through it [512]   */
   int32_t small_server; /* host-buffer products of at most 1024 words per operand (n <= 1024,
-                           q < 2^31, 32-bit words): 0 = served by a resident one-wave device
-                           kernel that polls a page-locked mailbox, the FPGA's GO / done-all
-                           handshake without a launch per call [automatic; the kernel leaves
-                           after 20 ms without a request and is relaunched on demand];
+                           q < 2^31, 32-bit words): 0 = served by a resident device kernel
+                           that polls a mailbox (go, a, b in device memory the host writes
+                           through its BAR mapping, or page-locked host memory without one; c
+                           in page-locked host memory), the FPGA's GO / done-all handshake
+                           without a launch per call [automatic; the kernel leaves after 20 ms
+                           without a request and is relaunched on demand];
                            -1 = a kernel launch per call                                        */
 } nttmul_params;
 
