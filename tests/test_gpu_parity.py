@@ -653,6 +653,30 @@ def test_small_server_two_wave_path(cyclic, torch_cuda):
             assert np.array_equal(got[0], exp), (q, cyclic, it)
 
 
+def test_small_server_two_contexts(torch_cuda):
+    """Two contexts in one process each run their own resident server (two kernels polling two
+    mailboxes at once): interleaved calls with different n and q stay exact, and destroying one
+    context (its server stopped) leaves the other serving."""
+    P1, P2 = O.Plan(256, Q0, 1002), O.Plan(512, Q31)
+    c1 = _ctx(256, Q0, psi=1002)
+    c2 = _ctx(512, Q31)
+    for it in range(30):
+        a1, b1 = O.fill_inputs(256, Q0, it, 1)
+        a2, b2 = O.fill_inputs(512, Q31, 1000 + it, 2)
+        g1 = c1.multiply(a1.astype(np.uint32), b1.astype(np.uint32)).astype(np.uint64)
+        g2 = c2.multiply(a2.astype(np.uint32), b2.astype(np.uint32)).astype(np.uint64)
+        assert c1.last_host_path() == 3 and c2.last_host_path() == 3
+        assert np.array_equal(g1[0], P1.product_merged(a1[0], b1[0])), it
+        for i in range(2):
+            assert np.array_equal(g2[i], P2.product_merged(a2[i], b2[i])), (it, i)
+    c1.close()
+    for it in range(5):
+        a2, b2 = O.fill_inputs(512, Q31, 2000 + it, 1)
+        g2 = c2.multiply(a2.astype(np.uint32), b2.astype(np.uint32)).astype(np.uint64)
+        assert c2.last_host_path() == 3
+        assert np.array_equal(g2[0], P2.product_merged(a2[0], b2[0])), it
+
+
 def test_small_server_answers_promptly(torch_cuda):
     """A request is answered while the server kernel keeps running, not when it leaves: 200
     back-to-back n = 256 products through the server take well under the 20 ms idle exit each

@@ -13,3 +13,6 @@ for i in 1 2 3; do
   timeout -k 10 120 $A tests/golden/coeficientes_a.txt tests/golden/coeficientes_b.txt 2000 > $OUT/time_testing_$i.txt 2>&1 || { tail -5 $OUT/time_testing_$i.txt; exit 1; }
   grep "us por" $OUT/time_testing_$i.txt
 done
+# one n = 1024 product (C1's shape) through the server, for the record
+timeout -k 10 120 python tools/r4/server_latency.py --n 1024 --q 2013265921 > $OUT/server_latency_1024.json 2> $OUT/server_latency_1024.err || { tail -20 $OUT/server_latency_1024.err; exit 1; }
+grep -A3 '"server"' $OUT/server_latency_1024.json; grep -A3 '"launch_per_call"' $OUT/server_latency_1024.json; grep compute_ns $OUT/server_latency_1024.json
