@@ -1045,13 +1045,14 @@ __device__ __forceinline__ void wide_inv(const KParams<Arith32P> &P, uint32_t (&
 // has changed from the pending marker).  The request half of the mailbox (req) is device memory
 // the host writes through its BAR mapping, so polls and operand loads stay on the device; c goes
 // to host memory (launch.hpp ServerReq / ServerBox).  n = 256, one product: the two-wave path
-// above.  Otherwise one wave runs the fused product of k_rows (64 / (n / 16) products per wave,
+// above; n = 1024: a and b transformed on two waves.  Otherwise one wave runs the fused product
+// of k_rows (64 / (n / 16) products per wave,
 // exchanges ordered per wave; a single product of n = 512 transforms a and b on two lane groups,
 // b's result handed to a's lanes by lane permutes).  It leaves on stop, after idle_ticks without
 // a request or after life_ticks in all (the host relaunches it on demand), so every wave always
 // ends -- the FPGA's GO / done-all handshake without a kernel launch per call.
 template <class A, int LOGS>
-__global__ __launch_bounds__(LOGS == 8 ? 128 : 64) void k_server(
+__global__ __launch_bounds__(LOGS == 9 ? 64 : 128) void k_server(
     KParams<A> P, const ServerReq *req, ServerBox *box, unsigned tw_pairs,
     unsigned long long idle_ticks, unsigned long long life_ticks) {
   using W = typename A::word;
@@ -1059,8 +1060,9 @@ __global__ __launch_bounds__(LOGS == 8 ? 128 : 64) void k_server(
   constexpr int N = Gr::N, TP = N / 16, PB = 64 / TP, G = Gr::G, NP = Gr::NP;
   static_assert(sizeof(W) == 4 && TP <= 64, "u32 words, n <= 1024");
   constexpr bool kWide = LOGS == 8 && IsPlantard<A>::value && NTTMUL_BASE_D && A::kBaseD == 2;
-  constexpr int KW = ServerBox::kWords, NT = LOGS == 8 ? 128 : 64;
-  __shared__ W lds[PB][NP];
+  constexpr bool kPair = LOGS == 10;  // n = 1024 (one product per request): a and b on two waves
+  constexpr int KW = ServerBox::kWords, NT = LOGS == 9 ? 64 : 128;
+  __shared__ W lds[PB < 2 ? 2 : PB][NP];
   __shared__ uint4 stg[2][KW / 4];  // a, b as loaded (c as stored reuses stg[0])
   __shared__ TwPair<W> twf[N], twi[N];  // launch_server: tw_pairs <= n
   __shared__ TwPair<W> wfu[kWide ? N : 1], wfs[kWide ? N : 1];
@@ -1165,6 +1167,66 @@ __global__ __launch_bounds__(LOGS == 8 ? 128 : 64) void k_server(
 #pragma unroll
           for (int i = 0; i < 4; i++)
             __builtin_amdgcn_raw_buffer_store_b32(x[i], rc, (lane + 64 * i) * 4, 0, 17);
+        }
+      }
+    } else if (kPair) {
+      if constexpr (kPair) {
+        // n = 1024: wave w loads operand w (system scope, through stg[w]) and runs the fused
+        // kernel's forward groups on it in its own LDS region -- the one-wave path transforms a
+        // and b on the same lanes, twice the instructions on one SIMD; wave 1 hands b's
+        // transform to wave 0's registers through LDS (same layout), and wave 0 runs the base
+        // multiplication and the inverse
+        {
+          const auto ro = span_rsrc(wave ? req->b : req->a, KW);
+          for (int i = lane; i < N / 4; i += 64) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(ro, i * 16, 0, 17);
+            stg[wave][i] = make_uint4(v[0], v[1], v[2], v[3]);
+          }
+        }
+        xsync<1>();
+        W x[16], y[16];
+        {
+          const W *src = (const W *)stg[wave];
+#pragma unroll
+          for (int k = 0; k < 16; k++) x[k] = src[Gr::base(0, j) + Gr::off(0, k)];
+        }
+#ifdef NTTMUL_CLOCK_STAMPS
+        st[1] = __builtin_amdgcn_s_memrealtime();
+        st[4] = __builtin_amdgcn_s_memtime();
+#endif
+        TwPair<W> zw[16];
+        W *lw = lds[wave];
+        fwd_all<A, LOGS, 0, 1, D, 1>(P.ar, x, y, lw, lw, P.fw, j, 0, 0, zw);
+        W *hand = (W *)stg[1];  // (b's input, already in wave 1's registers)
+        if (wave == 1) {
+#pragma unroll
+          for (int k = 0; k < 16; k++) hand[k * 64 + lane] = x[k];
+        }
+        __syncthreads();
+        if (wave == 0) {
+#pragma unroll
+          for (int k = 0; k < 16; k++) y[k] = hand[k * 64 + lane];
+          base_mult<A, LOGS, D>(P.ar, x, y, zw, j);
+          inv_all<A, LOGS, G - 1, true, D, 1>(P, x, y, lw, lw, P.iw, j, 0, 0);
+#ifdef NTTMUL_CLOCK_STAMPS
+          __builtin_amdgcn_sched_barrier(0);
+          st[2] = __builtin_amdgcn_s_memrealtime();
+          st[5] = __builtin_amdgcn_s_memtime();
+#endif
+          W *sc = (W *)stg[0];
+#pragma unroll
+          for (int k = 0; k < 16; k++) {
+            W v = x[k];
+            if (!A::kInvCanonical) v = P.ar.canon(v);
+            sc[Gr::base(0, j) + Gr::off(0, k)] = v;
+          }
+          xsync<1>();
+          const auto rc = span_rsrc(box->c, KW);  // (system-scope write-through, see below)
+          for (int i = lane; i < N / 4; i += 64) {
+            const uint4 v = stg[0][i];
+            __attribute__((ext_vector_type(4))) uint32_t w = {v.x, v.y, v.z, v.w};
+            __builtin_amdgcn_raw_buffer_store_b128(w, rc, i * 16, 0, 17);
+          }
         }
       }
     } else if (wave == 0) {
@@ -2180,7 +2242,7 @@ hipError_t launch_server(const LaunchTables &T, const ServerReq *req, ServerBox 
   switch (T.logn) {
     case 8: hipLaunchKernelGGL((k_server<Arith32P, 8>), dim3(1), dim3(128), 0, s, P, req, box, tp, idle_ticks, life_ticks); break;
     case 9: hipLaunchKernelGGL((k_server<Arith32P, 9>), dim3(1), dim3(64), 0, s, P, req, box, tp, idle_ticks, life_ticks); break;
-    default: hipLaunchKernelGGL((k_server<Arith32P, 10>), dim3(1), dim3(64), 0, s, P, req, box, tp, idle_ticks, life_ticks); break;
+    default: hipLaunchKernelGGL((k_server<Arith32P, 10>), dim3(1), dim3(128), 0, s, P, req, box, tp, idle_ticks, life_ticks); break;
   }
   return hipGetLastError();
 }
