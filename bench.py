@@ -24,6 +24,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "ntt-based-polynomial-multiplier-fpga_amd"))
 
 METRIC = "polymults/sec (n=4096, 32-bit q) at 1/2/4/8 MI355X; % HBM roofline"
+# --op: the product (the BASELINE metric) or one of SURVEY §8(f) row 1's standalone steps on
+# either side of it, measured the same way: (unit, words moved per polynomial / n)
+OPS = {"multiply": ("polymults/s", 3), "forward": ("forward NTTs/s", 2),
+       "inverse": ("inverse NTTs/s", 2), "pointwise": ("pointwise products/s", 3)}
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 SEED = 0x4E54544D554C
 
@@ -97,6 +101,10 @@ def parse(argv=None):
                     help="polymults per GPU per step, the same at every N (weak scaling; default "
                          "C3's 65536; C4 = --batch-per-gpu 131072 at 8 ranks: 2^20 in all)")
     ap.add_argument("--word-bits", type=int, default=0, help="32/64 coefficient storage (0: auto)")
+    ap.add_argument("--op", choices=sorted(OPS), default="multiply",
+                    help="multiply (the BASELINE metric); forward / inverse / pointwise time the "
+                         "standalone batched entry points (nttmul_forward/inverse/pointwise_batch_"
+                         "device, SURVEY 8(f) row 1) with the same contract, not the headline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-io", action="store_true",
                     help="also time the host-buffer ABI path (PCIe-inclusive; never the value)")
@@ -529,7 +537,8 @@ def main(argv=None):
     p0, p1 = shard(global_batch, rank, world)
     count = p1 - p0
     wbytes = wb // 8
-    alg_bytes = 3 * n * wbytes * count                    # read a, b + write c, per launch
+    unit, words = OPS[args.op]
+    alg_bytes = words * n * wbytes * count                # read a (and b) + write the result
     rotate = buffer_sets(alg_bytes, args.rotate)
     nstreams = max(1, args.streams)
     if nstreams > 1:  # each buffer set always goes to the same stream (no cross-stream reuse)
@@ -554,7 +563,14 @@ def main(argv=None):
         a, b, c = sets[state["i"] % rotate]
         st = streams[state["i"] % nstreams]
         state["i"] += 1
-        ctx.multiply_device(c, a, b, count, wb, stream=st.cuda_stream)
+        if args.op == "multiply":
+            ctx.multiply_device(c, a, b, count, wb, stream=st.cuda_stream)
+        elif args.op == "forward":
+            ctx.forward_device(c, a, count, wb, stream=st.cuda_stream)
+        elif args.op == "inverse":
+            ctx.inverse_device(c, a, count, wb, stream=st.cuda_stream)
+        else:
+            ctx.pointwise_device(c, a, b, count, wb, stream=st.cuda_stream)
 
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
@@ -590,14 +606,18 @@ def main(argv=None):
     if rank == 0:
         value = global_batch * args.steps / wall_max
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9     # GB/s
-        single_launch = n <= 4096
+        product = args.op == "multiply"
+        single_launch = n <= 4096 and product
         co = code_object_or_none()
-        traffic, traffic_source = load_traffic(n, q, count, co) if co else (None, "no code object")
+        traffic, traffic_source = (load_traffic(n, q, count, co) if co and product else
+                                   (None, "no code object" if not co else "PMC profiles are of the product"))
         resident = alg_bytes * rotate <= IC_BYTES
         line = {
-            "metric": METRIC,
+            "metric": METRIC if product else
+                      f"{unit[:-2]}/sec (n={n}, {'32' if wb == 32 else '64'}-bit words), standalone "
+                      "batched entry point (SURVEY 8(f) row 1; not the headline); % HBM roofline",
             "value": value,
-            "unit": "polymults/s",
+            "unit": unit,
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -611,15 +631,18 @@ def main(argv=None):
             "dtype": "u32" if wb == 32 else "u64",
             "data": "synthetic: splitmix64 counter-based coefficients mod q, generated on device "
                     "(SURVEY §8d, seed 0x4E54544D554C)",
-            "config": {"workload": f"{workload_name(n, q, global_batch, world)}: "
-                                   f"n={n}, q={q}, batch {batch} polymults per GPU "
+            "config": {"workload": (f"{workload_name(n, q, global_batch, world)}: " if product else
+                                    f"{args.op} on {workload_name(n, q, global_batch, world)}'s shape: ") +
+                                   f"n={n}, q={q}, batch {batch} polynomials per GPU "
                                    f"(global {global_batch}), device-resident",
+                       "op": args.op,
                        "n": n, "q": q, "batch_per_gpu": batch, "global_batch": global_batch,
                        "parallelism": f"batch shards x{world}, no collective"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": traffic_source,
-                         "kernel": ctx.last_kernel_name() or ctx.kernel_name(wb, count),
+                         "kernel": ((ctx.last_kernel_name() or ctx.kernel_name(wb, count)) if product
+                                    else f"nttmul_{args.op}_batch_device"),
                          "kernel_ms": kern_ms,
                          "alg_bytes_per_launch": alg_bytes,
                          "buffer_sets": rotate,
@@ -663,7 +686,7 @@ def main(argv=None):
                                             units_per_step=count)
             except Exception as e:  # reported evidence, never required
                 line["power"] = {"error": str(e)}
-        if world == 1 and args.clock_seconds > 0:
+        if world == 1 and args.clock_seconds > 0 and product:
             a, b, c = sets[0]
             try:
                 clk = diag_clock(n, q, wb, count, a, b, c, devno, sptr,
@@ -678,10 +701,10 @@ def main(argv=None):
                     vr["in_kernel_clock_ghz"] = g
                     vr["bound_ms_at_in_kernel_clock"] = vr["cycles_per_wave"] * vr["waves_per_simd"] / (g * 1e9) * 1e3
                     vr["frac_at_in_kernel_clock"] = vr["bound_ms_at_in_kernel_clock"] / kern_ms
-        if args.host_io:
+        if args.host_io and product:
             a, b, _ = sets[0]
             line["host_io"] = host_io(ctx, a, b, count, n, wb)
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and product:
             try:
                 line["cpu_baseline"] = cpu_baseline(n, q, args.cpu_seconds)
             except Exception as e:  # the baseline is reported, never required

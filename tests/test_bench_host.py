@@ -176,3 +176,15 @@ def test_settle_runs_untimed_chunks_until_the_wall_time():
     assert n < 200                # chunks stop doubling at 10 ms, so little overshoot
     assert t["syncs"] >= 5        # paced: never one unsynchronised burst
     assert bench.settle(step, 0, sync) == (0, 0.0)
+
+
+def test_op_defaults_to_the_product():
+    """The default step is the product (the BASELINE metric); --op forward / inverse / pointwise
+    time the standalone entry points with their own unit and bytes moved."""
+    assert bench.parse([]).op == "multiply"
+    assert bench.OPS["multiply"] == ("polymults/s", 3)
+    assert bench.OPS["forward"][1] == bench.OPS["inverse"][1] == 2   # read x, write its transform
+    assert bench.OPS["pointwise"][1] == 3
+    assert bench.parse(["--op", "inverse"]).op == "inverse"
+    with pytest.raises(SystemExit):
+        bench.parse(["--op", "square"])
