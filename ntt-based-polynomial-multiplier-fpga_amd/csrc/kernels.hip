@@ -1504,6 +1504,11 @@ __global__ __launch_bounds__(128) void k_rows_ab(KParams<A> P, const uint32_t *_
 //   DIR 1 (inverse): NTT/ntt.C:428-451 nttmul_gs_rev2std followed by the n^-1 scaling of
 //     ntt256.C:12 (P.f = n^-1 here), so inverse(forward(a)) == a; with L1 > 0 this is the row
 //     pass before k_cols_inv and the output stays lazy.
+// Forward transforms of 32-bit words with L1 == 0 take two polynomials per thread group (the
+// product kernel's a and b form: one twiddle load and one exchange barrier per stage serve both,
+// and twice the independent butterflies per lane).
+template <class A, int L1, int DIR>
+constexpr int xform_upg() { return DIR == 0 && L1 == 0 && sizeof(typename A::word) == 4 ? 2 : 1; }
 template <class A, class TIn, class TOut, int LOGS, int L1, int DIR>
 __global__ __launch_bounds__(256) void k_xform(KParams<A> P, const TIn *__restrict__ in,
                                                TOut *__restrict__ out, size_t units) {
@@ -1511,20 +1516,25 @@ __global__ __launch_bounds__(256) void k_xform(KParams<A> P, const TIn *__restri
   using Gr = Groups<LOGS, kWT<A, LOGS>()>;
   constexpr int N = Gr::N, TP = N / 16, PB = 256 / TP, G = Gr::G, NP = Gr::NP;
   constexpr int GIN = DIR == 0 ? 0 : G - 1, GOUT = DIR == 0 ? G - 1 : 0;
-  __shared__ W lds[PB][NP];
+  constexpr int UPG = xform_upg<A, L1, DIR>();
+  __shared__ W lds[PB][UPG][NP];
   const int pb = threadIdx.x / TP, j = threadIdx.x % TP;
-  const size_t u = (size_t)blockIdx.x * PB + pb;
-  const bool live = u < units;
+  const size_t u = ((size_t)blockIdx.x * PB + pb) * UPG;
+  const bool live = u < units, live2 = UPG == 2 && u + 1 < units;
   const int row = L1 ? (int)(u & ((1u << L1) - 1)) : 0;
   const size_t base_in = (live ? u : 0) * N + Gr::base(GIN, j);
+  const size_t base_in2 = (live2 ? u + 1 : live ? u : 0) * N + Gr::base(GIN, j);
   W x[16], y[16];
 #pragma unroll
-  for (int k = 0; k < 16; k++) x[k] = to_word<W>(in[base_in + Gr::off(GIN, k)]);
+  for (int k = 0; k < 16; k++) {
+    x[k] = to_word<W>(in[base_in + Gr::off(GIN, k)]);
+    if (UPG == 2) y[k] = to_word<W>(in[base_in2 + Gr::off(GIN, k)]);
+  }
   TwPair<W> zw[16];
   if (DIR == 0)
-    fwd_all<A, LOGS, 0, 1>(P.ar, x, y, lds[pb], lds[pb], P.fw, j, row, L1, zw);
+    fwd_all<A, LOGS, 0, UPG>(P.ar, x, y, lds[pb][0], lds[pb][UPG - 1], P.fw, j, row, L1, zw);
   else
-    inv_all<A, LOGS, G - 1, L1 == 0>(P, x, y, lds[pb], lds[pb], P.iw, j, row, L1);
+    inv_all<A, LOGS, G - 1, L1 == 0>(P, x, y, lds[pb][0], lds[pb][0], P.iw, j, row, L1);
   if (live) {
     const size_t base_out = u * N + Gr::base(GOUT, j);
 #pragma unroll
@@ -1533,6 +1543,11 @@ __global__ __launch_bounds__(256) void k_xform(KParams<A> P, const TIn *__restri
       if (DIR == 0 || (L1 == 0 && !A::kInvCanonical)) v = P.ar.canon(v);
       out[base_out + Gr::off(GOUT, k)] = (TOut)v;
     }
+  }
+  if (live2) {
+    const size_t base_out = (u + 1) * N + Gr::base(GOUT, j);
+#pragma unroll
+    for (int k = 0; k < 16; k++) out[base_out + Gr::off(GOUT, k)] = (TOut)P.ar.canon(y[k]);
   }
 }
 
@@ -2260,7 +2275,7 @@ hipError_t describe_polymul(const LaunchTables &T, int io_bits, size_t batch, st
 template <class A, class TIn, class TOut, int LOGS, int L1, int DIR>
 static hipError_t launch_xform_rows(const KParams<A> &P, const void *in, void *out, size_t units,
                                     hipStream_t s) {
-  constexpr int PB = 256 / ((1 << LOGS) / 16);
+  constexpr int PB = 256 / ((1 << LOGS) / 16) * xform_upg<A, L1, DIR>();
   const size_t blocks = (units + PB - 1) / PB;
   if (blocks == 0) return hipSuccess;
   hipLaunchKernelGGL((k_xform<A, TIn, TOut, LOGS, L1, DIR>), dim3((unsigned)blocks), dim3(256), 0,
