@@ -627,7 +627,9 @@ __device__ __forceinline__ void fwd_all(const A &ar, typename A::word (&x)[16],
   }
 }
 
-template <class A, int LOGS, int g, bool SCALE, int SKIP = 0, int SYNC = 0>
+// NPOLY 2 (standalone inverse transforms, k_xform): y is a second polynomial inverted alongside x
+// with the same twiddles (the product inverts one)
+template <class A, int LOGS, int g, bool SCALE, int SKIP = 0, int SYNC = 0, int NPOLY = 1>
 __device__ __forceinline__ void inv_all(const KParams<A> &P, typename A::word (&x)[16],
                                         typename A::word (&y)[16], typename A::word *lx,
                                         typename A::word *ly,
@@ -635,9 +637,10 @@ __device__ __forceinline__ void inv_all(const KParams<A> &P, typename A::word (&
                                         int row, int l1) {
   using Gr = Groups<LOGS, kWT<A, LOGS>()>;
   inv_group<A, LOGS, g, SCALE, g + 1 == Gr::G ? SKIP : 0>(P, x, tw, j, row, l1);
+  if constexpr (NPOLY == 2) inv_group<A, LOGS, g, SCALE, g + 1 == Gr::G ? SKIP : 0>(P, y, tw, j, row, l1);
   if constexpr (g > 0) {
-    exchange<LOGS, g, g - 1, 1, typename A::word, SYNC, kWT<A, LOGS>()>(x, y, lx, ly, j);
-    inv_all<A, LOGS, g - 1, SCALE, SKIP, SYNC>(P, x, y, lx, ly, tw, j, row, l1);
+    exchange<LOGS, g, g - 1, NPOLY, typename A::word, SYNC, kWT<A, LOGS>()>(x, y, lx, ly, j);
+    inv_all<A, LOGS, g - 1, SCALE, SKIP, SYNC, NPOLY>(P, x, y, lx, ly, tw, j, row, l1);
   }
 }
 
@@ -1504,11 +1507,11 @@ __global__ __launch_bounds__(128) void k_rows_ab(KParams<A> P, const uint32_t *_
 //   DIR 1 (inverse): NTT/ntt.C:428-451 nttmul_gs_rev2std followed by the n^-1 scaling of
 //     ntt256.C:12 (P.f = n^-1 here), so inverse(forward(a)) == a; with L1 > 0 this is the row
 //     pass before k_cols_inv and the output stays lazy.
-// Forward transforms of 32-bit words with L1 == 0 take two polynomials per thread group (the
-// product kernel's a and b form: one twiddle load and one exchange barrier per stage serve both,
-// and twice the independent butterflies per lane).
+// Transforms of 32-bit words with L1 == 0 take two polynomials per thread group (the product
+// kernel's a and b form: one twiddle load and one exchange barrier per stage serve both, and
+// twice the independent butterflies per lane).
 template <class A, int L1, int DIR>
-constexpr int xform_upg() { return DIR == 0 && L1 == 0 && sizeof(typename A::word) == 4 ? 2 : 1; }
+constexpr int xform_upg() { return L1 == 0 && sizeof(typename A::word) == 4 ? 2 : 1; }
 template <class A, class TIn, class TOut, int LOGS, int L1, int DIR>
 __global__ __launch_bounds__(256) void k_xform(KParams<A> P, const TIn *__restrict__ in,
                                                TOut *__restrict__ out, size_t units) {
@@ -1534,7 +1537,7 @@ __global__ __launch_bounds__(256) void k_xform(KParams<A> P, const TIn *__restri
   if (DIR == 0)
     fwd_all<A, LOGS, 0, UPG>(P.ar, x, y, lds[pb][0], lds[pb][UPG - 1], P.fw, j, row, L1, zw);
   else
-    inv_all<A, LOGS, G - 1, L1 == 0>(P, x, y, lds[pb][0], lds[pb][0], P.iw, j, row, L1);
+    inv_all<A, LOGS, G - 1, L1 == 0, 0, 0, UPG>(P, x, y, lds[pb][0], lds[pb][UPG - 1], P.iw, j, row, L1);
   if (live) {
     const size_t base_out = u * N + Gr::base(GOUT, j);
 #pragma unroll
@@ -1547,7 +1550,11 @@ __global__ __launch_bounds__(256) void k_xform(KParams<A> P, const TIn *__restri
   if (live2) {
     const size_t base_out = (u + 1) * N + Gr::base(GOUT, j);
 #pragma unroll
-    for (int k = 0; k < 16; k++) out[base_out + Gr::off(GOUT, k)] = (TOut)P.ar.canon(y[k]);
+    for (int k = 0; k < 16; k++) {
+      W v = y[k];
+      if (DIR == 0 || !A::kInvCanonical) v = P.ar.canon(v);
+      out[base_out + Gr::off(GOUT, k)] = (TOut)v;
+    }
   }
 }
 
