@@ -128,3 +128,89 @@ def test_wave_typed_layouts():
             types = {(Gr.base(g, j) >> bit) & 1 for j in range(64 * w, 64 * w + 64)}
             assert len(types) == 1 and types == {(w & 1)}
     assert sum(_extra_cycles(Gr, x, g) for x in range(2) for g in (x, x + 1)) == 0
+
+
+# --- the device server's two-wave n = 256 path (kernels.hip wl_elem / wl_swap_64 / wl_swap_42) ---
+
+def wl_elem(p, t, i):
+    """Element held by lane t, register i of layout p (register bits = element bits p, p + 1)."""
+    return (t & ((1 << p) - 1)) | ((t >> p) << (p + 2)) | (i << p)
+
+
+def permlane_swap(x, a, b, bit):
+    """v_permlane16_swap (bit 4) / v_permlane32_swap (bit 5) of registers a (vdst) and b (vsrc):
+    the lanes of a with the bit set trade places with the lanes of b with it clear."""
+    xa, xb = list(x[a]), list(x[b])
+    for t in range(64):
+        if t & (1 << bit):
+            xa[t], xb[t - (1 << bit)] = x[b][t - (1 << bit)], x[a][t]
+    x[a], x[b] = xa, xb
+
+
+def dpp_swap(x, a, b, sh):
+    """wl_swap_dpp<SH, A, B>: row_shr / row_shl by SH lanes inside 16-lane rows and two selects."""
+    up = [x[b][t - sh] if (t % 16) >= sh else 0 for t in range(64)]       # row_shr:SH of x[b]
+    dn = [x[a][t + sh] if (t % 16) + sh < 16 else 0 for t in range(64)]   # row_shl:SH of x[a]
+    x[a] = [up[t] if t & sh else x[a][t] for t in range(64)]
+    x[b] = [x[b][t] if t & sh else dn[t] for t in range(64)]
+
+
+def layout(p):
+    return [[wl_elem(p, t, i) for t in range(64)] for i in range(4)]
+
+
+def test_server_wide_layouts_are_bijections():
+    """Each layout of the two-wave path holds every one of the 256 elements exactly once, and the
+    LDS pad e + (e >> 5) stays inside the kernel's per-wave region (NP words at n = 256)."""
+    for p in (6, 4, 2, 0):
+        els = [e for reg in layout(p) for e in reg]
+        assert sorted(els) == list(range(256)), p
+    assert max(e + (e >> 5) for e in range(256)) < Groups(8).NP
+
+
+def test_server_wide_in_wave_swaps():
+    """The permlane and DPP sequences that replaced two LDS exchanges per transform move every
+    element exactly where the next layout expects it (layouts 6 <-> 4 and 4 <-> 2, both ways)."""
+    def swap_64(x):
+        permlane_swap(x, 0, 1, 4)
+        permlane_swap(x, 2, 3, 4)
+        permlane_swap(x, 0, 2, 5)
+        permlane_swap(x, 1, 3, 5)
+
+    def swap_42(x):
+        dpp_swap(x, 0, 1, 4)
+        dpp_swap(x, 2, 3, 4)
+        dpp_swap(x, 0, 2, 8)
+        dpp_swap(x, 1, 3, 8)
+
+    for f, src, dst in ((swap_64, 6, 4), (swap_64, 4, 6), (swap_42, 4, 2), (swap_42, 2, 4)):
+        x = layout(src)
+        f(x)
+        assert x == layout(dst), (src, dst)
+
+
+def test_server_wide_stage_pairs_and_twiddles():
+    """In every layout the butterfly partners of a stage sit in the register pairs the kernel
+    pairs (register bit 1 for a group's first stage, bit 0 for its second), and the twiddle entry
+    the kernel loads for each pair (kernels.hip wide_tw) is the reference table's entry for that
+    butterfly, 2^s + e >> (8 - s) with e the pair's lower element; the base block of lane t in
+    layout 0 takes stage 5's entry 32 + t / 2 and is a -w block exactly for odd t."""
+    def kernel_entry(s, t, pair_hi):  # wide_tw's index for stage s, the pair (0,1) or (2,3)/(1,3)
+        k3, k5 = 8 + ((t >> 4) << 1), 32 + ((t >> 2) << 1)
+        return {0: 1, 1: 2 + pair_hi, 2: 4 + (t >> 4), 3: k3 + pair_hi, 4: 16 + (t >> 2),
+                5: k5 + pair_hi}[s]
+    groups = {6: (0, 1), 4: (2, 3), 2: (4, 5)}
+    for p, (s0, s1) in groups.items():
+        for s, rbit in ((s0, 1), (s1, 0)):
+            d = 128 >> s
+            pairs = [(0, 2), (1, 3)] if rbit == 1 else [(0, 1), (2, 3)]
+            for t in range(64):
+                for hi, (i, j) in enumerate(pairs):
+                    e, f = wl_elem(p, t, i), wl_elem(p, t, j)
+                    assert f - e == d and not e & d, (p, s, t, i)
+                    # the second-of-group stages pick the entry by the pair, the first by the lane
+                    got = kernel_entry(s, t, hi if rbit == 0 else 0)
+                    assert got == (1 << s) + (e >> (8 - s)), (p, s, t, i, got)
+    for t in range(64):
+        e0 = wl_elem(0, t, 0)
+        assert e0 == 4 * t and 32 + (t >> 1) == 32 + (e0 >> 3) and ((e0 >> 2) & 1) == (t & 1)
