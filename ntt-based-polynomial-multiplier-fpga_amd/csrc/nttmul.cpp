@@ -582,8 +582,11 @@ int server_alloc(nttmul_ctx *ctx, DevState &d) {
     info.size = sizeof(info);
     ServerReq *hv = nullptr;
     if (hsa_amd_pointer_info(dv, &info, nullptr, nullptr, nullptr) == HSA_STATUS_SUCCESS &&
-        info.hostBaseAddress && info.agentBaseAddress == dv)
-      hv = (ServerReq *)info.hostBaseAddress;
+        info.hostBaseAddress && info.agentBaseAddress) {  // (dv may lie inside a larger block)
+      const size_t off = (size_t)((char *)dv - (char *)info.agentBaseAddress);
+      if (off + sizeof(ServerReq) <= info.sizeInBytes)
+        hv = (ServerReq *)((char *)info.hostBaseAddress + off);
+    }
     uint32_t back = 0;
     if (hv) {
       __atomic_store_n(&hv->go, 0x5A5A5A5Au, __ATOMIC_RELEASE);
