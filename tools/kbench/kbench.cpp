@@ -91,8 +91,21 @@ int main(int argc, char **argv) {
   if (sub) {
     for (int r = 0; r < 3; r++)
       for (int i = 0; i < 3; i++) CK(hipMalloc(&ring[r][i], sub * n * (P.word_bits / 8)));
-    CK(hipStreamCreateWithFlags(&scol, hipStreamNonBlocking));
-    CK(hipStreamCreateWithFlags(&srow, hipStreamNonBlocking));
+    // KB_COL_CUS=k: spatial partition instead of co-residency -- the column stream may use CUs
+    // [0, k), the row stream the others (hipExtStreamCreateWithCUMask; 0 = both use every CU)
+    const int col_cus = getenv("KB_COL_CUS") ? atoi(getenv("KB_COL_CUS")) : 0;
+    if (col_cus > 0) {
+      int ncu = 0;
+      CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+      std::vector<uint32_t> mc((ncu + 31) / 32, 0), mr((ncu + 31) / 32, 0);
+      for (int cu = 0; cu < ncu; cu++) (cu < col_cus ? mc : mr)[cu / 32] |= 1u << (cu % 32);
+      CK(hipExtStreamCreateWithCUMask(&scol, (uint32_t)mc.size(), mc.data()));
+      CK(hipExtStreamCreateWithCUMask(&srow, (uint32_t)mr.size(), mr.data()));
+      printf("  column stream on CUs [0, %d), row stream on [%d, %d)\n", col_cus, col_cus, ncu);
+    } else {
+      CK(hipStreamCreateWithFlags(&scol, hipStreamNonBlocking));
+      CK(hipStreamCreateWithFlags(&srow, hipStreamNonBlocking));
+    }
     for (int i = 0; i < kEv; i++) {
       CK(hipEventCreateWithFlags(&evcf[i], hipEventDisableTiming));
       CK(hipEventCreateWithFlags(&evr[i], hipEventDisableTiming));
