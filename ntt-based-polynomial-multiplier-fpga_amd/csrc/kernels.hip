@@ -1047,15 +1047,15 @@ __device__ __forceinline__ void wide_inv(const KParams<Arith32P> &P, uint32_t (&
 // in system-scope write-through stores (the host takes the request as done when every word of c
 // has changed from the pending marker).  The request half of the mailbox (req) is device memory
 // the host writes through its BAR mapping, so polls and operand loads stay on the device; c goes
-// to host memory (launch.hpp ServerReq / ServerBox).  n = 256, one product: the two-wave path
-// above; n = 1024: a and b transformed on two waves.  Otherwise one wave runs the fused product
+// to host memory (launch.hpp ServerReq / ServerBox).  n = 256: the two-wave path above, one pair
+// of waves per product of the request (up to 4); n = 1024: a and b transformed on two waves.  Otherwise one wave runs the fused product
 // of k_rows (64 / (n / 16) products per wave,
 // exchanges ordered per wave; a single product of n = 512 transforms a and b on two lane groups,
 // b's result handed to a's lanes by lane permutes).  It leaves on stop, after idle_ticks without
 // a request or after life_ticks in all (the host relaunches it on demand), so every wave always
 // ends -- the FPGA's GO / done-all handshake without a kernel launch per call.
 template <class A, int LOGS>
-__global__ __launch_bounds__(LOGS == 9 ? 64 : 128) void k_server(
+__global__ __launch_bounds__(LOGS == 8 ? 512 : LOGS == 9 ? 64 : 128) void k_server(
     KParams<A> P, const ServerReq *req, ServerBox *box, unsigned tw_pairs,
     unsigned long long idle_ticks, unsigned long long life_ticks) {
   using W = typename A::word;
@@ -1064,8 +1064,8 @@ __global__ __launch_bounds__(LOGS == 9 ? 64 : 128) void k_server(
   static_assert(sizeof(W) == 4 && TP <= 64, "u32 words, n <= 1024");
   constexpr bool kWide = LOGS == 8 && IsPlantard<A>::value && NTTMUL_BASE_D && A::kBaseD == 2;
   constexpr bool kPair = LOGS == 10;  // n = 1024 (one product per request): a and b on two waves
-  constexpr int KW = ServerBox::kWords, NT = LOGS == 9 ? 64 : 128;
-  __shared__ W lds[PB < 2 ? 2 : PB][NP];
+  constexpr int KW = ServerBox::kWords, NT = LOGS == 8 ? 512 : LOGS == 9 ? 64 : 128;
+  __shared__ W lds[kWide ? 2 * PB : PB < 2 ? 2 : PB][NP];
   __shared__ uint4 stg[2][KW / 4];  // a, b as loaded (c as stored reuses stg[0])
   __shared__ TwPair<W> twf[N], twi[N];  // launch_server: tw_pairs <= n
   __shared__ TwPair<W> wfu[kWide ? N : 1], wfs[kWide ? N : 1];
@@ -1121,52 +1121,59 @@ __global__ __launch_bounds__(LOGS == 9 ? 64 : 128) void k_server(
     const unsigned long long now = __builtin_amdgcn_s_memrealtime();
     const int count = (int)(go & 0xFFu);
     if (count == (int)ServerBox::kStop || count > PB) break;  // stop (count > PB: never posted)
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the host's a, b before go
+    // the host's a, b before go (only the waves that load them: on the n = 256 path eight waves
+    // invalidating at once cost a single product 0.5 us)
+    if (!kWide || (wave >> 1) < count) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 #ifdef NTTMUL_CLOCK_STAMPS
     unsigned long long st[6];
     st[0] = __builtin_amdgcn_s_memrealtime();
 #endif
     const int q4 = count * (N / 4);  // 16-byte quads per operand (count <= PB, so <= KW / 4)
-    if (kWide && count == 1) {
+    if (kWide) {
       if constexpr (kWide) {
-        // wave w loads operand w in layout 6 (system scope: the host's writes reach memory
-        // behind any cached copy) and transforms it
+        // product p = wave / 2 of the request (count <= 4): wave 2p loads and transforms a_p,
+        // wave 2p + 1 b_p (layout 6, system-scope loads: the host's writes reach memory behind
+        // any cached copy); waves of products past count only keep the barriers
+        const int prod = wave >> 1, opnd = wave & 1;
+        const bool mine = prod < count;
         uint32_t x[4];
-        const auto ro = span_rsrc(wave ? req->b : req->a, KW);
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-          x[i] = __builtin_amdgcn_raw_buffer_load_b32(ro, (lane + 64 * i) * 4, 0, 17);
-#ifdef NTTMUL_CLOCK_STAMPS
-        __builtin_amdgcn_s_waitcnt(0);
-        st[1] = __builtin_amdgcn_s_memrealtime();
-        st[4] = __builtin_amdgcn_s_memtime();
-#endif
         uint32_t *lw = lds[wave];
-        wide_fwd(P.ar, x, wtw, lw, lane);
-        // both transforms to the block layout (one 4-coefficient base block per lane of wave 0)
+        if (mine) {
+          const auto ro = span_rsrc((opnd ? req->b : req->a) + prod * N, N);
 #pragma unroll
-        for (int i = 0; i < 4; i++) lw[wl_pad(wl_elem<2>(lane, i))] = x[i];
+          for (int i = 0; i < 4; i++)
+            x[i] = __builtin_amdgcn_raw_buffer_load_b32(ro, (lane + 64 * i) * 4, 0, 17);
+#ifdef NTTMUL_CLOCK_STAMPS
+          __builtin_amdgcn_s_waitcnt(0);
+          st[1] = __builtin_amdgcn_s_memrealtime();
+          st[4] = __builtin_amdgcn_s_memtime();
+#endif
+          wide_fwd(P.ar, x, wtw, lw, lane);
+          // both transforms to the block layout (one 4-coefficient base block per lane)
+#pragma unroll
+          for (int i = 0; i < 4; i++) lw[wl_pad(wl_elem<2>(lane, i))] = x[i];
+        }
         __syncthreads();
-        if (wave == 0) {
+        if (mine && opnd == 0) {
           uint32_t y[4];
 #pragma unroll
           for (int i = 0; i < 4; i++) {
-            x[i] = lds[0][wl_pad(wl_elem<0>(lane, i))];
-            y[i] = lds[1][wl_pad(wl_elem<0>(lane, i))];
+            x[i] = lds[wave][wl_pad(wl_elem<0>(lane, i))];
+            y[i] = lds[wave + 1][wl_pad(wl_elem<0>(lane, i))];
           }
           xsync<1>();
           // block lane: elements 4 lane .. 4 lane + 3, a residue mod x^4 -+ w with w the stage-5
           // entry 32 + lane / 2, minus for odd lanes (the stage's differences)
           P.ar.basemul4_lane(x, y, wtw.z.w, wtw.z.ws, lane & 1);
-          wl_exchange<0, 2>(x, lds[0], lane);
-          wide_inv(P, x, wtw, lds[0], lane);
+          wl_exchange<0, 2>(x, lw, lane);
+          wide_inv(P, x, wtw, lw, lane);
 #ifdef NTTMUL_CLOCK_STAMPS
           __builtin_amdgcn_sched_barrier(0);
           st[2] = __builtin_amdgcn_s_memrealtime();
           st[5] = __builtin_amdgcn_s_memtime();
 #endif
           // (the host watches c itself, see below: system-scope write-through stores)
-          const auto rc = span_rsrc(box->c, KW);
+          const auto rc = span_rsrc(box->c + prod * N, N);
 #pragma unroll
           for (int i = 0; i < 4; i++)
             __builtin_amdgcn_raw_buffer_store_b32(x[i], rc, (lane + 64 * i) * 4, 0, 17);
@@ -2262,7 +2269,7 @@ hipError_t launch_server(const LaunchTables &T, const ServerReq *req, ServerBox 
   const KParams<Arith32P> P = product_params<Arith32P>(T);
   const unsigned tp = (unsigned)pairs;
   switch (T.logn) {
-    case 8: hipLaunchKernelGGL((k_server<Arith32P, 8>), dim3(1), dim3(128), 0, s, P, req, box, tp, idle_ticks, life_ticks); break;
+    case 8: hipLaunchKernelGGL((k_server<Arith32P, 8>), dim3(1), dim3(512), 0, s, P, req, box, tp, idle_ticks, life_ticks); break;
     case 9: hipLaunchKernelGGL((k_server<Arith32P, 9>), dim3(1), dim3(64), 0, s, P, req, box, tp, idle_ticks, life_ticks); break;
     default: hipLaunchKernelGGL((k_server<Arith32P, 10>), dim3(1), dim3(128), 0, s, P, req, box, tp, idle_ticks, life_ticks); break;
   }

@@ -16,3 +16,6 @@ done
 # one n = 1024 product (C1's shape) through the server, for the record
 timeout -k 10 120 python tools/r4/server_latency.py --n 1024 --q 2013265921 > $OUT/server_latency_1024.json 2> $OUT/server_latency_1024.err || { tail -20 $OUT/server_latency_1024.err; exit 1; }
 grep -A3 '"server"' $OUT/server_latency_1024.json; grep -A3 '"launch_per_call"' $OUT/server_latency_1024.json; grep compute_ns $OUT/server_latency_1024.json
+# four n = 256 products per request (one pair of waves each)
+timeout -k 10 120 python tools/r4/server_latency.py --batch 4 > $OUT/server_latency_b4.json 2> $OUT/server_latency_b4.err || { tail -20 $OUT/server_latency_b4.err; exit 1; }
+grep -A3 '"server"' $OUT/server_latency_b4.json; grep compute_ns $OUT/server_latency_b4.json

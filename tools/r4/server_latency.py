@@ -20,16 +20,18 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--calls", type=int, default=2000)
 ap.add_argument("--n", type=int, default=256)
 ap.add_argument("--q", type=int, default=12289)
+ap.add_argument("--batch", type=int, default=1, help="products per call (n x batch <= 1024)")
 args = ap.parse_args()
 rng = np.random.default_rng(7)
-a = rng.integers(0, args.q, args.n, dtype=np.uint32)
-b = rng.integers(0, args.q, args.n, dtype=np.uint32)
-res = {"n": args.n, "q": args.q, "calls": args.calls}
+shape = args.n if args.batch == 1 else (args.batch, args.n)
+a = rng.integers(0, args.q, shape, dtype=np.uint32)
+b = rng.integers(0, args.q, shape, dtype=np.uint32)
+res = {"n": args.n, "q": args.q, "batch": args.batch, "calls": args.calls}
 outs = {}
 
 
 def timed(ctx, calls):
-    c = np.empty(args.n, np.uint32)
+    c = np.empty(shape, np.uint32)
     ctx.multiply(a, b, out=c)
     ts = []
     for _ in range(calls):
