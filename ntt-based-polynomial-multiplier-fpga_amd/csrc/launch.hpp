@@ -25,27 +25,10 @@ struct LaunchTables {
   int prio = 0;            // nttmul_params.issue_prio: -1 never, 0 automatic, 1 always
   int prio_ok = 1;         // 0: the previous product launch of this context went to another
                            // stream, so automatic mode keeps oldest-first issue (kernels.hip rows_prio)
-  // tools/kbench builds only (the library never sets them):
-  int mp_lag = 0;            // n > 4096: > 0 = one persistent launch (k_mp_persist) with this
-                             // many steps between a polynomial's column, row and inverse tasks
-  void *mp_stats = nullptr;  // NTTMUL_MP_STATS builds: 9 u64 task statistics
-  int mp_phase = -1;         // n > 4096: -1 all three passes, 0 only k_cols_fwd, 1 only the row
-                             // pass, 2 only k_cols_inv (sub-batch pipelines across streams)
-  int rows_lds_extra = 0;    // n > 4096: dynamic LDS bytes added to each row-pass workgroup (caps
-                             // the row pass's workgroups per CU, leaving room for column waves)
-  int pipe_per_wave = 0;     // tools/kbench builds, n = 1024, q < 2^31, u32: > 0 = k_rows_pipe with this many products
-                             // per wave (loads of the next one issued before the current one's
-                             // transforms); 0 = one product per one-wave workgroup (k_rows)
 };
 
-#ifdef NTTMUL_KBENCH_BUILD
-// Bytes of the ticket / counter words k_mp_persist needs for `batch` polynomials (scr[3]).
-inline size_t mp_sync_bytes(size_t batch) { return (2 * batch + 2) * sizeof(unsigned); }
-#endif
-
 // c = a * b for `batch` polynomials of n = 2^logn words of io_bits (32/64) each, on stream s.
-// scr: three device buffers of batch * n words of word_bits, used only when n > 4096 (kbench
-// builds: a fourth of mp_sync_bytes(batch) for the persistent form, T.mp_lag > 0).
+// scr: three device buffers of batch * n words of word_bits, used only when n > 4096.
 hipError_t launch_polymul(const LaunchTables &T, const void *a, const void *b, void *c,
                           size_t batch, int io_bits, void **scr, hipStream_t s);
 // The kernels launch_polymul would launch for (T, io_bits), as "k_rows<Arith32P3,u32,u32,12,0>"

@@ -100,13 +100,14 @@ def test_no_device_host_alloc():
     assert ei.value.status == nttmul.NTTMUL_ENODEV
 
 
-@pytest.mark.parametrize("flag", ["NTTMUL_ABL_NOLOAD", "NTTMUL_ABL_NOXCHG", "NTTMUL_ABL_NOSTORE",
-                                  "NTTMUL_ABL_TWMASK", "NTTMUL_KBENCH_LITE", "NTTMUL_ABL_L2LOAD",
-                                  "NTTMUL_ABL_BOUNDQ", "NTTMUL_ABL_PERMXCHG", "NTTMUL_STAGGER",
-                                  "NTTMUL_ABL_L2CI", "NTTMUL_ABL_L2CF"])
-def test_ablation_switches_refuse_library_build(flag):
-    """The wrong-result kbench ablation switches cannot reach libnttmul.so: kernels.hip stops with
-    #error unless NTTMUL_KBENCH_BUILD is also defined (tools/kbench/build.sh only)."""
+@pytest.mark.parametrize("hook", ["NTTMUL_HOOK_ROWS_LD(b,u,N,b0)=0", "NTTMUL_HOOK_ROWS_ST(b,u,N,b0)=0",
+                                  "NTTMUL_HOOK_ROWS_INPUT(x,y,u,j)=", "NTTMUL_HOOK_ROWS_OUTPUT(x,c,b,l)=",
+                                  "NTTMUL_HOOK_XCHG()=", "NTTMUL_HOOK_COLS_LD(b,p,s,c,d)=0",
+                                  "NTTMUL_HOOK_COLS_ST(b,p,s,c)=0"])
+def test_instrumentation_hooks_refuse_library_build(hook):
+    """The wrong-result pricing variants live in tools/kbench (kb_kernels.hip defines the
+    NTTMUL_HOOK_* points of csrc/kernels_dev.hpp); the library's translation unit kernels.hip
+    stops with #error if any hook arrives defined, so none can reach libnttmul.so."""
     src = os.path.join(nttmul.PKG_DIR, "csrc", "kernels.hip")
     inc = ["-I" + os.path.join(nttmul.PKG_DIR, "csrc"),
            "-I" + os.path.join(os.path.dirname(nttmul.PKG_DIR), "include")]
@@ -114,8 +115,18 @@ def test_ablation_switches_refuse_library_build(flag):
            "-o", os.devnull]
     if not os.path.exists(cmd[0]):
         pytest.skip("hipcc not present")
-    bad = subprocess.run(cmd + [f"-D{flag}=1"], capture_output=True, text=True)
-    assert bad.returncode != 0 and "wrong-result kbench switches" in bad.stderr
-    ok = subprocess.run(cmd + [f"-D{flag}=1", "-DNTTMUL_KBENCH_BUILD=1"], capture_output=True,
-                        text=True)
+    bad = subprocess.run(cmd + [f"-D{hook}"], capture_output=True, text=True)
+    assert bad.returncode != 0 and "instrumentation points" in bad.stderr
+    ok = subprocess.run(cmd, capture_output=True, text=True)
     assert ok.returncode == 0, ok.stderr[-2000:]
+
+
+def test_product_sources_hold_no_kbench_code():
+    """Verdict r4 item 4: the rejected kernels (k_mp_persist, k_rows_w4 / _pipe / _ab) and the
+    ablation switches moved to tools/kbench; the product sources name none of them."""
+    csrc = os.path.join(nttmul.PKG_DIR, "csrc")
+    for name in os.listdir(csrc):
+        text = open(os.path.join(csrc, name), encoding="utf-8").read()
+        for banned in ("NTTMUL_KBENCH", "NTTMUL_ABL_", "k_mp_persist", "k_rows_w4", "k_rows_pipe",
+                       "k_rows_ab", "mp_lag", "pipe_per_wave", "rows_lds_extra"):
+            assert banned not in text, (name, banned)

@@ -5,17 +5,11 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <vector>
+
+#include "kb.hpp"
 #include "launch.hpp"
 #include "planner.hpp"
-#ifdef NTTMUL_WAVE_TRACE
-#include <algorithm>
-#include <vector>
-#include <map>
-namespace nttmul {
-hipError_t read_wave_trace(void *dst, size_t bytes);
-hipError_t read_wave_slots(void *dst, size_t bytes);
-}
-#endif
 
 #define CK(x)                                                                   \
   do {                                                                          \
@@ -42,7 +36,7 @@ int main(int argc, char **argv) {
   CK(hipMemcpy(iw, P.iw.data(), P.iw.size(), hipMemcpyHostToDevice));
   if (P.logn > 12) {
     for (int i = 0; i < 3; i++) CK(hipMalloc(&scr[i], batch * n * (P.word_bits / 8)));
-    CK(hipMalloc(&scr[3], nttmul::mp_sync_bytes(batch)));
+    CK(hipMalloc(&scr[3], kb::mp_sync_bytes(batch)));
   }
   nttmul::LaunchTables T;
   T.logn = P.logn; T.word_bits = P.word_bits; T.q = P.q; T.qinv_neg = P.qinv_neg;
@@ -51,18 +45,20 @@ int main(int argc, char **argv) {
   T.f8 = P.f8; T.f8s = P.f8s; T.wf8 = P.wf8; T.wf8s = P.wf8s;
   T.fi = P.fi; T.fis = P.fis; T.wfi = P.wfi; T.wfis = P.wfis; T.r2 = P.r2;
   CK(hipDeviceGetAttribute(&T.cus, hipDeviceAttributeMultiprocessorCount, 0));
+  kb::Conf C;
   // KB_MP_LAG > 0: n > 4096 products as one persistent launch (k_mp_persist) with this lag
-  T.mp_lag = getenv("KB_MP_LAG") ? atoi(getenv("KB_MP_LAG")) : 0;
-  // KB_PIPE > 0: n = 1024 products through k_rows_pipe with KB_PIPE products per wave
-  T.pipe_per_wave = getenv("KB_PIPE") ? atoi(getenv("KB_PIPE")) : 0;
-  if (T.mp_lag > 0 && P.logn > 12) CK(hipMemset(scr[3], 0, nttmul::mp_sync_bytes(batch)));
+  C.mp_lag = getenv("KB_MP_LAG") ? atoi(getenv("KB_MP_LAG")) : 0;
+  // KB_PIPE: n = 1024 products through k_rows_pipe with KB_PIPE products per wave (> 0),
+  // k_rows_w4 (-1) or k_rows_ab (-2)
+  C.pipe_per_wave = getenv("KB_PIPE") ? atoi(getenv("KB_PIPE")) : 0;
+  if (C.mp_lag > 0 && P.logn > 12) CK(hipMemset(scr[3], 0, kb::mp_sync_bytes(batch)));
   unsigned long long *stats = nullptr;
 #if NTTMUL_MP_STATS
   CK(hipMalloc(&stats, 9 * 8));
   CK(hipMemset(stats, 0, 9 * 8));
-  T.mp_stats = stats;
+  C.mp_stats = stats;
 #endif
-  CK(nttmul::launch_fill(a, b, P.logn, q, 0x4E54544D554Cull, 0, batch, io_bits, 0));
+  CK(kb::fill(a, b, P.logn, q, 0x4E54544D554Cull, batch, io_bits, 0));
   // KB_ROTATE=R: the timed launches cycle over R (a, b, c) sets with identical inputs, so a batch
   // smaller than the 256 MiB Infinity Cache is read from HBM (as bench.py --rotate)
   const int rot = getenv("KB_ROTATE") ? atoi(getenv("KB_ROTATE")) : 1;
@@ -70,11 +66,11 @@ int main(int argc, char **argv) {
   ra[0] = a; rb[0] = b; rc[0] = c;
   for (int i = 1; i < rot && i < 64; i++) {
     CK(hipMalloc(&ra[i], bytes)); CK(hipMalloc(&rb[i], bytes)); CK(hipMalloc(&rc[i], bytes));
-    CK(nttmul::launch_fill(ra[i], rb[i], P.logn, q, 0x4E54544D554Cull, 0, batch, io_bits, 0));
+    CK(kb::fill(ra[i], rb[i], P.logn, q, 0x4E54544D554Cull, batch, io_bits, 0));
   }
   // KB_ROWS_LDS=B: the row pass of an n > 4096 product takes B more bytes of LDS per workgroup
   // (caps its workgroups per CU, so column-pass waves can be resident beside it)
-  T.rows_lds_extra = getenv("KB_ROWS_LDS") ? atoi(getenv("KB_ROWS_LDS")) : 0;
+  C.rows_lds_extra = getenv("KB_ROWS_LDS") ? atoi(getenv("KB_ROWS_LDS")) : 0;
   // KB_SUB=S (n > 4096): the batch runs as sub-batches of S products through a ring of three
   // scratch sets, the row passes on one stream and the column passes on another, issued so that
   // the columns of sub-batch i + 1 and the inverse columns of i - 1 can overlap the rows of i
@@ -114,10 +110,11 @@ int main(int argc, char **argv) {
   auto pipelined = [&](void *pa, void *pb, void *pc) {
     const size_t ns = batch / sub, step = sub * n * wb;
     auto pass = [&](int phase, size_t g, size_t i, hipStream_t s) {
-      nttmul::LaunchTables t = T;
-      t.mp_phase = phase;
-      CK(nttmul::launch_polymul(t, (char *)pa + i * step, (char *)pb + i * step,
-                                (char *)pc + i * step, sub, io_bits, ring[g % 3], s));
+      kb::Conf c = C;
+      c.mp_phase = phase;
+      void *r4[4] = {ring[g % 3][0], ring[g % 3][1], ring[g % 3][2], nullptr};
+      CK(kb::launch(T, c, (char *)pa + i * step, (char *)pb + i * step, (char *)pc + i * step,
+                    sub, io_bits, r4, s));
     };
     pass(0, gsub, 0, scol);
     CK(hipEventRecord(evcf[gsub % kEv], scol));
@@ -140,7 +137,7 @@ int main(int argc, char **argv) {
     for (int i = 0; i < 3; i++) pipelined(a, b, c);
     CK(hipDeviceSynchronize());
   } else {
-    for (int i = 0; i < 3; i++) CK(nttmul::launch_polymul(T, a, b, c, batch, io_bits, scr, 0));
+    for (int i = 0; i < 3; i++) CK(kb::launch(T, C, a, b, c, batch, io_bits, scr, 0));
   }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
@@ -175,10 +172,10 @@ int main(int argc, char **argv) {
     const int k = nstreams == 2 ? (i & 1) : 0;
     if (rot > 1) {
       const int r = i % (rot < 64 ? rot : 64);
-      CK(nttmul::launch_polymul(T, ra[r], rb[r], rc[r], batch, io_bits, scr, st[k]));
+      CK(kb::launch(T, C, ra[r], rb[r], rc[r], batch, io_bits, scr, st[k]));
       continue;
     }
-    CK(nttmul::launch_polymul(T, a, b, k ? c2 : c, batch, io_bits, scr, st[k]));
+    CK(kb::launch(T, C, a, b, k ? c2 : c, batch, io_bits, scr, st[k]));
   }
   if (nstreams == 2) {
     CK(hipEventRecord(join, st[1]));
@@ -201,66 +198,8 @@ int main(int argc, char **argv) {
     for (size_t i = 0; i < cnt; i++) sum = sum * 1099511628211ull + h[i];
     free(h);
   }
-#ifdef NTTMUL_WAVE_TRACE
-  {  // phase percentiles of the last launch (us from the first wave's entry)
-    const size_t nw = batch < 16384 ? batch : 16384;
-    std::vector<unsigned long long> tr(nw * 4);
-    CK(nttmul::read_wave_trace(tr.data(), tr.size() * 8));
-    unsigned long long t0 = ~0ull;
-    for (size_t i = 0; i < nw; i++) t0 = std::min(t0, tr[i * 4]);
-    const char *nm[4] = {"entry", "loaded", "computed", "stored"};
-    for (int k = 0; k < 4; k++) {
-      std::vector<double> v(nw);
-      for (size_t i = 0; i < nw; i++) v[i] = (tr[i * 4 + k] - t0) * 0.01;
-      std::sort(v.begin(), v.end());
-      printf("  %-9s p0 %6.2f  p10 %6.2f  p50 %6.2f  p90 %6.2f  p100 %6.2f us\n", nm[k], v[0],
-             v[nw / 10], v[nw / 2], v[nw * 9 / 10], v[nw - 1]);
-    }
-    // waves per SIMD (HW_ID bits 4-5 SIMD, 8-11 CU, 12 SH, 13-15 SE; XCC_ID << 24), and per
-    // SIMD load: when its last wave stored, against how many waves it ran
-    std::vector<unsigned> slot(nw);
-    CK(nttmul::read_wave_slots(slot.data(), slot.size() * 4));
-    std::map<unsigned, std::vector<size_t>> simd;
-    for (size_t i = 0; i < nw; i++) simd[slot[i] & 0xF00FF30u].push_back(i);
-    std::map<size_t, std::vector<double>> by_count;  // waves on the SIMD -> its last store (us)
-    std::map<unsigned, int> per_cu;
-    for (auto &kv : simd) {
-      double last = 0;
-      for (size_t i : kv.second) last = std::max(last, (tr[i * 4 + 3] - t0) * 0.01);
-      by_count[kv.second.size()].push_back(last);
-      per_cu[kv.first & 0xF00FF00u] += (int)kv.second.size();
-    }
-    printf("  SIMDs used %zu, CUs used %zu\n", simd.size(), per_cu.size());
-    for (auto &kv : by_count) {
-      std::sort(kv.second.begin(), kv.second.end());
-      printf("  %zu waves on %zu SIMDs: last store p0 %6.2f p50 %6.2f p100 %6.2f us\n", kv.first,
-             kv.second.size(), kv.second[0], kv.second[kv.second.size() / 2], kv.second.back());
-    }
-    std::map<int, int> cu_hist;
-    for (auto &kv : per_cu) cu_hist[kv.second]++;
-    printf("  waves per CU:");
-    for (auto &kv : cu_hist) printf(" %d x%d", kv.first, kv.second);
-    printf("\n");
-    // within the SIMDs holding 4 waves: completion order by entry order (oldest-first issue?)
-    std::vector<double> rank_done[8];
-    for (auto &kv : simd) {
-      if (kv.second.size() != 4) continue;
-      std::vector<size_t> w = kv.second;
-      std::sort(w.begin(), w.end(), [&](size_t x, size_t y) { return tr[x * 4] < tr[y * 4]; });
-      for (size_t r = 0; r < w.size(); r++)
-        rank_done[r].push_back((tr[w[r] * 4 + 2] - tr[w[r] * 4 + 1]) * 0.01);
-    }
-    for (int r = 0; r < 4; r++) {
-      auto &v = rank_done[r];
-      if (v.empty()) continue;
-      std::sort(v.begin(), v.end());
-      printf("  4-wave SIMDs, wave %d by entry: compute (loaded->computed) p50 %6.2f us\n", r,
-             v[v.size() / 2]);
-    }
-  }
-#endif
   unsigned fault = 0;
-  if (T.mp_lag > 0 && P.logn > 12) CK(hipMemcpy(&fault, (unsigned *)scr[3] + 1, 4, hipMemcpyDeviceToHost));
+  if (C.mp_lag > 0 && P.logn > 12) CK(hipMemcpy(&fault, (unsigned *)scr[3] + 1, 4, hipMemcpyDeviceToHost));
   if (fault) printf("FAULT: k_mp_persist poll gave up\n");
   if (stats) {
     unsigned long long h[9];
