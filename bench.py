@@ -90,6 +90,36 @@ def max_over_ranks(x: float, dist, device=None) -> float:
     return float(t.item())
 
 
+def gather_ranks(row, dist):
+    """Every rank's row of floats, in rank order (gloo all_gather of a CPU tensor); [row] when
+    not distributed."""
+    import torch
+    t = torch.tensor(row, dtype=torch.float64)
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return [list(row)]
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [x.tolist() for x in out]
+
+
+def rank_summary(rows, steps: int, bytes_per_unit: int, world: int, wall_max: float):
+    """Per-rank rates (units per second over each rank's own timed wall time, and over its
+    event-timed kernel time) and the aggregate roofline of the whole job: every rank's
+    algorithmic bytes over the max-over-ranks wall time, against N x the HBM peak (a slow rank
+    shows here, not in rank 0's event-timed roofline.frac)."""
+    rates = [cnt * steps / wall for wall, _, cnt in rows]
+    kern_rates = [cnt / (kms * 1e-3) for _, kms, cnt in rows]
+    total_bytes = sum(cnt for _, _, cnt in rows) * bytes_per_unit * steps
+    achieved = total_bytes / wall_max / 1e9
+    return ({"achieved": achieved, "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
+             "frac": achieved / (HBM_PEAK_GBS * world),
+             "source": "all ranks' algorithmic bytes over the max-over-ranks wall time of the K "
+                       "timed steps, against N x 8 TB/s"},
+            {"rates": rates, "min": min(rates), "max": max(rates),
+             "kernel_rates": kern_rates, "kernel_ms": [kms for _, kms, _ in rows],
+             "unit": "units/s per rank (own wall time; kernel_rates: own HIP-event kernel time)"})
+
+
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -593,6 +623,7 @@ def main(argv=None):
                        (lambda: dist.barrier()) if world > 1 else (lambda: None))
     kern_ms = ev0.elapsed_time(ev1) / args.steps
     wall_max = max_over_ranks(wall, dist if world > 1 else None)
+    rank_rows = gather_ranks([wall, kern_ms, float(count)], dist if world > 1 else None)
 
     if args.dump_samples:  # sampled products of this rank's slice, at their global positions
         import numpy as np
@@ -603,6 +634,10 @@ def main(argv=None):
         np.savez(f"{args.dump_samples}.rank{rank}.npz", p0=p0, p1=p1, idx=np.array(idx),
                  c=rows, n=n, q=q, world=world, global_batch=global_batch)
 
+    if world > 1:
+        # every rank's GPU work is done: rank 0 alone goes on to the CPU baseline (the others
+        # leave), so its sample runs on a quiet host at every N
+        dist.barrier()
     if rank == 0:
         value = global_batch * args.steps / wall_max
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9     # GB/s
@@ -651,6 +686,9 @@ def main(argv=None):
             "build": {"code_object": co},
             "cpu_baseline": None,
         }
+        agg, per_rank = rank_summary(rank_rows, args.steps, words * n * wbytes, world, wall_max)
+        line["roofline"]["aggregate"] = agg
+        line["ranks"] = per_rank
         if nstreams > 1:
             line["roofline"]["streams_note"] = (
                 f"consecutive steps alternate over {nstreams} HIP streams; kernel_ms is the time "
@@ -704,14 +742,17 @@ def main(argv=None):
         if args.host_io and product:
             a, b, _ = sets[0]
             line["host_io"] = host_io(ctx, a, b, count, n, wb)
-        if world == 1 and not args.no_cpu_baseline and product:
-            try:
+        if not args.no_cpu_baseline and product:
+            try:  # rank 0 only, after every rank's GPU work (the final barrier above)
                 line["cpu_baseline"] = cpu_baseline(n, q, args.cpu_seconds)
+                if line["cpu_baseline"] and world > 1:
+                    line["cpu_baseline"]["note"] = (
+                        f"rank 0 of {world}, after the final barrier: the other ranks have left, "
+                        "so the sample has the host to itself")
             except Exception as e:  # the baseline is reported, never required
                 line["cpu_baseline"] = {"error": str(e)}
         print(json.dumps(line), flush=True)
     if world > 1:
-        dist.barrier()
         dist.destroy_process_group()
 
 

@@ -62,8 +62,9 @@ typedef struct {
                           own host thread; <= 0 = all visible devices                           */
   int first_dev;       /* first HIP device index used                                           */
   uint32_t flags;      /* NTTMUL_FLAG_*                                                          */
-  /* Dispatch and runtime knobs, read once by nttmul_create_ex (0 = the default in brackets; a
-   * zero-initialised struct gets every default).  The library reads no environment variable. */
+  /* Dispatch and runtime knobs, read once by nttmul_create_sized (0 = the default in brackets; a
+   * zero-initialised struct gets every default; nttmul_create_ex reads the six fields above only
+   * and gives these their defaults).  The library reads no environment variable. */
   int32_t issue_prio;   /* fused products (n <= 4096, q < 2^31): 0 = automatic [the issue-
                            prioritised kernel for launches of at most 4 waves per SIMD made on the
                            same stream as the context's previous product launch], 1 = always,
@@ -79,10 +80,13 @@ typedef struct {
                            that polls a mailbox (go, a, b in device memory the host writes
                            through its BAR mapping, or page-locked host memory without one; c
                            in page-locked host memory), the FPGA's GO / done-all handshake
-                           without a launch per call [automatic; the kernel leaves after 20 ms
-                           without a request and is relaunched on demand];
+                           without a launch per call [automatic; the kernel leaves after 1 ms
+                           without a request (50 ms in all) and is relaunched on demand; it also
+                           leaves before the context enqueues any other work];
                            -1 = a kernel launch per call                                        */
 } nttmul_params;
+/* Bytes of the round 1-3 nttmul_params (n .. flags): what nttmul_create_ex reads. */
+#define NTTMUL_PARAMS_BASE_SIZE offsetof(nttmul_params, issue_prio)
 
 typedef struct {
   uint32_t n, logn;
@@ -95,7 +99,12 @@ typedef struct {
 
 /* ≙ PCIE_Load + PCIE_Open + mode-0 parameter/twiddle stream (NTT_PCIECommunicationv2.c:137-178) */
 int nttmul_create(nttmul_ctx **ctx, uint32_t n, uint64_t q, int ndev);
+/* the fields n .. flags of *params (NTTMUL_PARAMS_BASE_SIZE bytes); the knobs take defaults */
 int nttmul_create_ex(nttmul_ctx **ctx, const nttmul_params *params);
+/* the first params_size bytes of *params, the rest defaults: pass sizeof(nttmul_params) to set
+ * the knobs.  NTTMUL_EINVAL for params_size below NTTMUL_PARAMS_BASE_SIZE or above the size this
+ * library knows (fields it could not honour). */
+int nttmul_create_sized(nttmul_ctx **ctx, const nttmul_params *params, size_t params_size);
 /* ≙ PCIE_Close + PCIE_Unload */
 void nttmul_destroy(nttmul_ctx *ctx);
 

@@ -27,6 +27,12 @@
 #ifndef NTTMUL_SPLIT16
 #define NTTMUL_SPLIT16 4
 #endif
+// 64-bit words at n = 65536 (C5): the square split 256 x 256 (kernels_dev.hpp k_cols8; 8 column
+// stages in the HBM-bound column passes, 8 in the row pass) instead of NTTMUL_SPLIT16's.  The
+// 32-bit classes keep NTTMUL_SPLIT16 (their twiddle typing, p_signed_fw_entry, follows it)
+#ifndef NTTMUL_C5_SQ
+#define NTTMUL_C5_SQ 1
+#endif
 // Arith32P forward CT typing: 0 = off; 1 = a difference x - t stays signed when its next use in
 // the register group is as an X; 2 = every in-group difference stays signed and is multiplied by
 // the signed-input Plantard product, so the planner stores those forward twiddles in signed form

@@ -54,9 +54,40 @@ static hipError_t multipass_l1(const LaunchTables &T, const void *a, const void 
 }
 
 
+// Multi-pass product of the square split, n = 65536 = 256 x 256 (64-bit words, NTTMUL_C5_SQ):
+// k_cols8 forward (global stages 0..7 of a and b), the row pass k_rows<..., 8, 8> (stages 8..15,
+// base multiplication, inverse stages 15..8 of 256-coefficient rows), k_cols8 inverse.
+template <class A, class IO>
+static hipError_t multipass_sq(const LaunchTables &T, const void *a, const void *b, void *c,
+                               size_t batch, void *ta, void *tb, void *tc, hipStream_t s) {
+  using W = typename A::word;
+  const KParams<A> P = product_params<A>(T);
+  const size_t groups = batch * 16;  // 16 workgroups of 16 columns per polynomial
+  if (tl_describe) {
+    const std::string args = std::string(AName<A>::v) + "," + word_name<IO>();
+    describe_add("k_cols8<" + args + ",fwd>");
+    (void)launch_rows<A, W, W, 8, 8>(P, ta, tb, tc, batch << 8, s);
+    describe_add("k_cols8<" + args + ",inv>");
+    return hipSuccess;
+  }
+  if (groups == 0) return hipSuccess;
+  hipLaunchKernelGGL((k_cols8<A, IO, W, 0>), dim3((unsigned)groups), dim3(256), 0, s, P,
+                     (const IO *)a, (const IO *)b, (W *)ta, (W *)tb, groups);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  e = launch_rows<A, W, W, 8, 8>(P, ta, tb, tc, batch << 8, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((k_cols8<A, W, IO, 1>), dim3((unsigned)groups), dim3(256), 0, s, P,
+                     (const W *)tc, (const W *)nullptr, (IO *)c, (IO *)nullptr, groups);
+  return hipGetLastError();
+}
+
 template <class A, class IO>
 static hipError_t multipass(const LaunchTables &T, const void *a, const void *b, void *c,
                             size_t batch, void **scr, hipStream_t s) {
+  if constexpr (sizeof(typename A::word) == 8 && NTTMUL_C5_SQ) {
+    if (T.logn == 16) return multipass_sq<A, IO>(T, a, b, c, batch, scr[0], scr[1], scr[2], s);
+  }
   switch (T.logn) {
     case 13: return multipass_l1<A, IO, 1>(T, a, b, c, batch, scr[0], scr[1], scr[2], s);
     case 14: return multipass_l1<A, IO, 2>(T, a, b, c, batch, scr[0], scr[1], scr[2], s);

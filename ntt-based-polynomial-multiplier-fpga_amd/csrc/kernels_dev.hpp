@@ -526,44 +526,47 @@ __device__ __forceinline__ void xsync() {
 }
 
 
-// Move 16 registers of each region from layout gfrom to layout gto through LDS.
-template <int LOGS, int gfrom, int gto, int NREG, class W, int SYNC = 0, bool WT = false>
+// Move 16 registers of each region from layout gfrom to layout gto through LDS.  ES: LDS words
+// between consecutive (padded) elements of one polynomial (1; k_cols8 interleaves the 16 column
+// transforms of a workgroup element by element, ES = 16, so a wave's lanes on adjacent columns
+// touch adjacent words).
+template <int LOGS, int gfrom, int gto, int NREG, class W, int SYNC = 0, bool WT = false, int ES = 1>
 __device__ __forceinline__ void exchange(W (&x)[16], W (&y)[16], W *lds_x, W *lds_y, int j) {
   using Gr = Groups<LOGS, WT>;
   NTTMUL_HOOK_XCHG();
   constexpr int X = gfrom < gto ? gfrom : gto;
-  const int bw = Gr::template padx<X>(Gr::base(gfrom, j));
-  const int br = Gr::template padx<X>(Gr::base(gto, j));
+  const int bw = Gr::template padx<X>(Gr::base(gfrom, j)) * ES;
+  const int br = Gr::template padx<X>(Gr::base(gto, j)) * ES;
   if (lds_regions<W>() == 1 && NREG == 2) {  // one region, the two polynomials in turn
 #pragma unroll
-    for (int k = 0; k < 16; k++) lds_x[bw + Gr::template padx<X>(Gr::off(gfrom, k))] = x[k];
+    for (int k = 0; k < 16; k++) lds_x[bw + Gr::template padx<X>(Gr::off(gfrom, k)) * ES] = x[k];
     xsync<SYNC>();
 #pragma unroll
-    for (int k = 0; k < 16; k++) x[k] = lds_x[br + Gr::template padx<X>(Gr::off(gto, k))];
+    for (int k = 0; k < 16; k++) x[k] = lds_x[br + Gr::template padx<X>(Gr::off(gto, k)) * ES];
     xsync<SYNC>();
 #pragma unroll
-    for (int k = 0; k < 16; k++) lds_x[bw + Gr::template padx<X>(Gr::off(gfrom, k))] = y[k];
+    for (int k = 0; k < 16; k++) lds_x[bw + Gr::template padx<X>(Gr::off(gfrom, k)) * ES] = y[k];
     xsync<SYNC>();
 #pragma unroll
-    for (int k = 0; k < 16; k++) y[k] = lds_x[br + Gr::template padx<X>(Gr::off(gto, k))];
+    for (int k = 0; k < 16; k++) y[k] = lds_x[br + Gr::template padx<X>(Gr::off(gto, k)) * ES];
     xsync<SYNC>();
     return;
   }
 #pragma unroll
   for (int k = 0; k < 16; k++) {
-    lds_x[bw + Gr::template padx<X>(Gr::off(gfrom, k))] = x[k];
-    if (NREG == 2) lds_y[bw + Gr::template padx<X>(Gr::off(gfrom, k))] = y[k];
+    lds_x[bw + Gr::template padx<X>(Gr::off(gfrom, k)) * ES] = x[k];
+    if (NREG == 2) lds_y[bw + Gr::template padx<X>(Gr::off(gfrom, k)) * ES] = y[k];
   }
   xsync<SYNC>();
 #pragma unroll
   for (int k = 0; k < 16; k++) {
-    x[k] = lds_x[br + Gr::template padx<X>(Gr::off(gto, k))];
-    if (NREG == 2) y[k] = lds_y[br + Gr::template padx<X>(Gr::off(gto, k))];
+    x[k] = lds_x[br + Gr::template padx<X>(Gr::off(gto, k)) * ES];
+    if (NREG == 2) y[k] = lds_y[br + Gr::template padx<X>(Gr::off(gto, k)) * ES];
   }
   xsync<SYNC>();
 }
 
-template <class A, int LOGS, int g, int NPOLY = 2, int SKIP = 0, int SYNC = 0>
+template <class A, int LOGS, int g, int NPOLY = 2, int SKIP = 0, int SYNC = 0, int ES = 1>
 __device__ __forceinline__ void fwd_all(const A &ar, typename A::word (&x)[16],
                                         typename A::word (&y)[16], typename A::word *lx,
                                         typename A::word *ly,
@@ -573,14 +576,15 @@ __device__ __forceinline__ void fwd_all(const A &ar, typename A::word (&x)[16],
   constexpr bool last = g + 1 == Gr::G;
   fwd_group<A, LOGS, g, NPOLY, last ? SKIP : 0>(ar, x, y, tw, j, row, l1, zw);
   if constexpr (!last) {
-    exchange<LOGS, g, g + 1, NPOLY, typename A::word, SYNC, kWT<A, LOGS>()>(x, y, lx, ly, j);
-    fwd_all<A, LOGS, g + 1, NPOLY, SKIP, SYNC>(ar, x, y, lx, ly, tw, j, row, l1, zw);
+    exchange<LOGS, g, g + 1, NPOLY, typename A::word, SYNC, kWT<A, LOGS>(), ES>(x, y, lx, ly, j);
+    fwd_all<A, LOGS, g + 1, NPOLY, SKIP, SYNC, ES>(ar, x, y, lx, ly, tw, j, row, l1, zw);
   }
 }
 
 // NPOLY 2 (standalone inverse transforms, k_xform): y is a second polynomial inverted alongside x
 // with the same twiddles (the product inverts one)
-template <class A, int LOGS, int g, bool SCALE, int SKIP = 0, int SYNC = 0, int NPOLY = 1>
+template <class A, int LOGS, int g, bool SCALE, int SKIP = 0, int SYNC = 0, int NPOLY = 1,
+          int ES = 1>
 __device__ __forceinline__ void inv_all(const KParams<A> &P, typename A::word (&x)[16],
                                         typename A::word (&y)[16], typename A::word *lx,
                                         typename A::word *ly,
@@ -590,8 +594,8 @@ __device__ __forceinline__ void inv_all(const KParams<A> &P, typename A::word (&
   inv_group<A, LOGS, g, SCALE, g + 1 == Gr::G ? SKIP : 0>(P, x, tw, j, row, l1);
   if constexpr (NPOLY == 2) inv_group<A, LOGS, g, SCALE, g + 1 == Gr::G ? SKIP : 0>(P, y, tw, j, row, l1);
   if constexpr (g > 0) {
-    exchange<LOGS, g, g - 1, NPOLY, typename A::word, SYNC, kWT<A, LOGS>()>(x, y, lx, ly, j);
-    inv_all<A, LOGS, g - 1, SCALE, SKIP, SYNC, NPOLY>(P, x, y, lx, ly, tw, j, row, l1);
+    exchange<LOGS, g, g - 1, NPOLY, typename A::word, SYNC, kWT<A, LOGS>(), ES>(x, y, lx, ly, j);
+    inv_all<A, LOGS, g - 1, SCALE, SKIP, SYNC, NPOLY, ES>(P, x, y, lx, ly, tw, j, row, l1);
   }
 }
 
@@ -665,6 +669,16 @@ __device__ __forceinline__ void base_mult(const A &ar, typename A::word (&x)[16]
 __host__ __device__ constexpr int rows_threads(int logs) {
   return NTTMUL_SMALL_BLOCK && logs == 10 ? 64 : 256;
 }
+// Square split (k_cols8): the intermediates ta, tb, tc tiled per 16 columns (NTTMUL_C5_TILE), so
+// the column passes store / load one contiguous 32 KiB tile per workgroup and the row pass moves
+// 512 contiguous bytes per instruction, instead of 128-byte runs 2 KiB apart (a row-major
+// column) on the column side
+#ifndef NTTMUL_C5_TILE
+#define NTTMUL_C5_TILE 1
+#endif
+__host__ __device__ constexpr bool c8_tile(int logs, int l1) {
+  return NTTMUL_C5_TILE && logs == 8 && l1 == 8;
+}
 
 // Fused product of `units` independent rows of 2^LOGS coefficients.
 //   L1 == 0 : each unit is a whole polynomial (n = 2^LOGS): full product, canonical output.
@@ -713,7 +727,12 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
   const size_t u = (size_t)blockIdx.x * PB + pb;
   const bool live = u < units;
   const int row = L1 ? (int)(u & ((1u << L1) - 1)) : 0;
-  const size_t base_g = u * N + Gr::base(0, j);
+  // (the square split's intermediates are tiled, c8_tile: row u = (p, m) keeps its element e at
+  // p 2^16 + (e >> 4) 2^12 + 16 m + (e & 15), i.e. register k of lane j at 4096 k + 16 m + j)
+  constexpr bool kTile = c8_tile(LOGS, L1);
+  constexpr int kRS = kTile ? 256 : 1;  // word stride of Gr::off(0, k)
+  const size_t base_g = kTile ? ((u >> 8) << 16) + ((u & 255) << 4) + Gr::base(0, j)
+                              : u * N + Gr::base(0, j);
   // threads past the batch end read unit 0 (always valid) instead of branching per load; their
   // results are never stored
   const size_t base_l = live ? base_g : (size_t)Gr::base(0, j);
@@ -752,8 +771,8 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
   } else {
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-      x[k] = to_word<W>(ld_stream<kNT>(a + base_r + Gr::off(0, k)));
-      y[k] = to_word<W>(ld_stream<kNT>(b + base_r + Gr::off(0, k)));
+      x[k] = to_word<W>(ld_stream<kNT>(a + base_r + Gr::off(0, k) * kRS));
+      y[k] = to_word<W>(ld_stream<kNT>(b + base_r + Gr::off(0, k) * kRS));
     }
   }
   NTTMUL_HOOK_ROWS_INPUT(x, y, u, j);
@@ -790,7 +809,7 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
     for (int k = 0; k < 16; k++) {
       W v = x[k];
       if (L1 == 0 && !A::kInvCanonical) v = P.ar.canon(v);
-      st_stream<kNT>(c + base_w + Gr::off(0, k), (TOut)v);
+      st_stream<kNT>(c + base_w + Gr::off(0, k) * kRS, (TOut)v);
     }
   }
   CLK_STAMP(1);
@@ -1364,6 +1383,68 @@ __global__ __launch_bounds__(256) void k_cols_inv(KParams<A> P,
   for (int m = 0; m < M; m++)
     st_stream<NTTMUL_NT_COLS>(c + base + ((size_t)m << logs),
                               (TOut)(A::kInvCanonical ? x[m] : P.ar.canon(x[m])));
+}
+
+// Column pass of the square split n = 2^8 x 2^8 (n = 65536, NTTMUL_C5_SQ): each column of 256
+// coefficients (stride 256 words) is a 256-point transform of global stages 0..7, run like one
+// k_rows row of Groups<8> (16 coefficients per thread, two register groups of four stages, one LDS
+// exchange) on the column's elements m = 0..255 (address m * 256 + column).  A 256-thread
+// workgroup takes 16 adjacent columns: thread t = 16 jj + cl runs register-group position jj of
+// column cl, so every load and store instruction moves 4 rows x 16 columns (128-B runs for u64),
+// and the 16 transforms share the LDS element by element (word 16 padx(e) + cl: conflict-free for
+// ds_write_b64's 16-lane and ds_read_b64's 32-lane groups).  Against the 16 x 4096
+// split the VALU-bound row pass sheds half of its butterflies to these passes, which are HBM-bound
+// and had VALU issue to spare.
+//   DIR 0: global stages 0..7 of the forward CT on a and b (twiddles P.fw[1 .. 255], uniform over
+//          the columns); X of stage 0 canonical by contract; output lazy, in place of the column
+//   DIR 1: global stages 7..0 of the inverse GS with F folded into stage 0; canonical output
+template <class A, class TIn, class TOut, int DIR>
+__global__ __launch_bounds__(256) void k_cols8(KParams<A> P, const TIn *__restrict__ a,
+                                               const TIn *__restrict__ b, TOut *__restrict__ ta,
+                                               TOut *__restrict__ tb, size_t groups) {
+  using W = typename A::word;
+  using Gr = Groups<8>;
+  constexpr int CW = 16, G = Gr::G, NPOLY = DIR == 0 ? 2 : 1;
+  constexpr int GIN = DIR == 0 ? 0 : G - 1, GOUT = DIR == 0 ? G - 1 : 0;
+  static_assert(G == 2 && Gr::NP * CW >= (Gr::padx<0>(255) + 1) * CW, "Groups<8> layout");
+  __shared__ W lds[Gr::NP * CW];
+  const size_t g = blockIdx.x;
+  if (g >= groups) return;  // (grid = groups exactly; block-uniform)
+  const int cl = threadIdx.x % CW, jj = threadIdx.x / CW;
+  const size_t p = g >> 4;
+  const size_t base = (p << 16) + ((g & 15) << 4) + cl;  // element m of the column at base + 256 m
+  // the intermediate side (DIR 0 stores, DIR 1 loads): with c8_tile the workgroup's 16 columns
+  // are one contiguous 4096-word tile, element m of column cl at 16 m + cl
+  constexpr bool kTile = c8_tile(8, 8);
+  const size_t ibase = kTile ? (p << 16) + ((g & 15) << 12) + cl : base;
+  constexpr int kIS = kTile ? 4 : 8;  // log2 word stride of m on the intermediate side
+  const size_t base_r = NTTMUL_HOOK_COLS_LD(DIR == 0 ? base : ibase, p, 16, ((g & 15) << 4) + cl, DIR);
+  W x[16], y[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const size_t o = (size_t)(Gr::base(GIN, jj) + Gr::off(GIN, k)) << (DIR == 0 ? 8 : kIS);
+    x[k] = (W)ld_stream<NTTMUL_NT_COLS>(a + base_r + o);
+    y[k] = NPOLY == 2 ? (W)ld_stream<NTTMUL_NT_COLS>(b + base_r + o) : W(0);
+  }
+  if constexpr (DIR == 0) {
+    TwPair<W> zw[16];
+    fwd_all<A, 8, 0, 2, 0, 0, CW>(P.ar, x, y, lds + cl, lds + cl, P.fw, jj, 0, 0, zw);
+    const size_t base_w = NTTMUL_HOOK_COLS_ST(ibase, p, 16, ((g & 15) << 4) + cl);
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const size_t o = (size_t)(Gr::base(GOUT, jj) + Gr::off(GOUT, k)) << kIS;
+      st_stream<NTTMUL_NT_COLS>(ta + base_w + o, (TOut)x[k]);
+      st_stream<NTTMUL_NT_COLS>(tb + base_w + o, (TOut)y[k]);
+    }
+  } else {
+    inv_all<A, 8, G - 1, true, 0, 0, 1, CW>(P, x, y, lds + cl, lds + cl, P.iw, jj, 0, 0);
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const size_t o = (size_t)(Gr::base(GOUT, jj) + Gr::off(GOUT, k)) << 8;
+      st_stream<NTTMUL_NT_COLS>(ta + base + o,
+                                (TOut)(A::kInvCanonical ? x[k] : P.ar.canon(x[k])));
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -92,10 +92,14 @@ struct Server {
   bool running = false;                       // launched and not known to have left
   std::chrono::steady_clock::time_point launched, last_done;
 };
-constexpr unsigned long long kServerIdleTicks = 2000000;  // 20 ms at 100 MHz (s_memrealtime)
-constexpr unsigned long long kServerLifeTicks = 100000000; // 1 s
-constexpr auto kServerIdleHost = std::chrono::milliseconds(10);   // host-side margins: past
-constexpr auto kServerLifeHost = std::chrono::milliseconds(500);  // these, stop and relaunch
+// The resident kernel occupies its hardware queue (4 per process on the box) while it waits, so
+// work other streams place in that queue -- and a device-wide synchronize -- waits behind it.  It
+// therefore stays only briefly: 1 ms without a request, 50 ms in all (then the next call
+// relaunches it, ~20 us), and the context stops it before it enqueues any other work (advisor r4).
+constexpr unsigned long long kServerIdleTicks = 100000;    // 1 ms at 100 MHz (s_memrealtime)
+constexpr unsigned long long kServerLifeTicks = 5000000;   // 50 ms
+constexpr auto kServerIdleHost = std::chrono::microseconds(500);  // host-side margins: past
+constexpr auto kServerLifeHost = std::chrono::milliseconds(25);   // these, stop and relaunch
 
 }  // namespace
 
@@ -329,12 +333,17 @@ class CopyPool {
   // split over at most `threads` threads (the caller's included)
   void copy(void *dst, const void *src, size_t bytes, unsigned threads) {
     const size_t kPart = 1u << 20;
-    const size_t parts = std::min<size_t>(std::min<size_t>(workers_ + 1, threads), bytes / kPart);
+    size_t parts = std::min<size_t>(std::min<size_t>(cap_, threads), bytes / kPart);
     if (parts <= 1) {
       memcpy(dst, src, bytes);
       return;
     }
     std::unique_lock<std::mutex> call(call_mu_);  // one split copy at a time
+    parts = std::min<size_t>(parts, grow((unsigned)parts - 1) + 1);
+    if (parts <= 1) {
+      memcpy(dst, src, bytes);
+      return;
+    }
     const size_t step = (bytes / parts + 4095) & ~(size_t)4095;
     {
       std::lock_guard<std::mutex> l(mu_);
@@ -343,30 +352,43 @@ class CopyPool {
       bytes_ = bytes;
       step_ = step;
       pending_ = parts - 1;
-      used_ = parts - 1;
-      gen_++;
+      for (size_t i = 0; i + 1 < parts; i++) w_[i].go = true;
     }
-    cv_.notify_all();
+    // wake exactly the workers this copy uses (each waits on its own condition variable)
+    for (size_t i = 0; i + 1 < parts; i++) w_[i].cv.notify_one();
     memcpy(dst, src, std::min(step, bytes));
     std::unique_lock<std::mutex> l(mu_);
     done_.wait(l, [&] { return pending_ == 0; });
   }
 
  private:
+  struct Worker {
+    std::condition_variable cv;
+    bool go = false;
+  };
   CopyPool() {
-    // kMaxCopyThreads - 1 workers at most (the host's hardware threads bound it); each call
-    // uses its context's params.copy_threads of them
     const unsigned hw = std::thread::hardware_concurrency();
-    workers_ = std::min(kMaxCopyThreads, std::max(hw, 1u)) - 1;
-    for (unsigned i = 0; i < workers_; i++) std::thread([this, i] { run(i); }).detach();
+    cap_ = std::min(kMaxCopyThreads, std::max(hw, 1u));
+  }
+  // Workers start on first use, up to the largest split any context has asked for (advisor r4:
+  // not min(64, hardware threads) - 1 of them up front); returns how many are running.
+  unsigned grow(unsigned want) {
+    while (started_ < want && started_ + 1 < kMaxCopyThreads) {
+      try {
+        const unsigned i = started_;
+        std::thread([this, i] { run(i); }).detach();
+        started_++;
+      } catch (...) {  // no thread available: split over the ones running
+        break;
+      }
+    }
+    return std::min(started_, want);
   }
   void run(unsigned i) {
-    unsigned seen = 0;
+    std::unique_lock<std::mutex> l(mu_);
     for (;;) {
-      std::unique_lock<std::mutex> l(mu_);
-      cv_.wait(l, [&] { return gen_ != seen; });
-      seen = gen_;
-      if (i >= used_) continue;
+      w_[i].cv.wait(l, [&] { return w_[i].go; });
+      w_[i].go = false;
       const size_t o = (i + 1) * step_;
       char *d = d_;
       const char *s = s_;
@@ -377,11 +399,11 @@ class CopyPool {
       if (--pending_ == 0) done_.notify_one();
     }
   }
-  unsigned workers_ = 0;
+  Worker w_[kMaxCopyThreads];
+  unsigned cap_ = 1, started_ = 0;  // started_: guarded by call_mu_
   std::mutex call_mu_, mu_;
-  std::condition_variable cv_, done_;
-  unsigned gen_ = 0;
-  size_t pending_ = 0, used_ = 0, bytes_ = 0, step_ = 0;
+  std::condition_variable done_;
+  size_t pending_ = 0, bytes_ = 0, step_ = 0;
   char *d_ = nullptr;
   const char *s_ = nullptr;
 };
@@ -610,12 +632,28 @@ int server_alloc(nttmul_ctx *ctx, DevState &d) {
   return NTTMUL_OK;
 }
 
+// The context's server leaves before the context enqueues anything else (run_device, the launch
+// path of run_host, fills): its kernel would otherwise hold that work's hardware queue until its
+// idle exit.
+int server_quiesce(nttmul_ctx *ctx) { return ctx->server.running ? server_stop(ctx) : NTTMUL_OK; }
+
+// The server cannot run for this context (setup or launch refused, e.g. no fine-grained memory
+// or an unsupported table): every later small call takes the launch path.
+int server_unavailable(nttmul_ctx *ctx) {
+  ctx->small_server = -1;
+  ctx->server.running = false;
+  (void)hipGetLastError();
+  ctx->err[0] = 0;
+  return 1;
+}
+
 // >0: not served here (the caller takes the launch path); else a status
 int run_server(nttmul_ctx *ctx, void *c, const void *a, const void *b, size_t batch) {
   const Plan &P = ctx->plan;
   const size_t words = batch * P.n;
   if (ctx->small_server < 0 || ctx->ndev != 1 || P.word_bits != 32 || P.logn < 8 || P.logn > 10 ||
-      words > (size_t)ServerBox::kWords || a32_kind(P.q) != A32Kind::Plantard)
+      words > (size_t)ServerBox::kWords || a32_kind(P.q) != A32Kind::Plantard ||
+      P.fw.size() / 8 > P.n)  // (launch_server copies n twiddle pairs of 2 x u32 into LDS)
     return 1;
   if (ctx->flags & NTTMUL_FLAG_VALIDATE) {  // the range check of run_device, on the host
     const uint32_t *pa = (const uint32_t *)a, *pb = (const uint32_t *)b;
@@ -627,19 +665,13 @@ int run_server(nttmul_ctx *ctx, void *c, const void *a, const void *b, size_t ba
   }
   Server &S = ctx->server;
   DevState &d = ctx->dev[0];
-  if (!S.req) {
-    const int st = server_alloc(ctx, d);
-    if (st) return st;
-  }
+  if (!S.req && server_alloc(ctx, d)) return server_unavailable(ctx);
   const auto now = std::chrono::steady_clock::now();
   if (S.running && (now - S.last_done > kServerIdleHost || now - S.launched > kServerLifeHost)) {
     const int st = server_stop(ctx);
     if (st) return st;
   }
-  if (!S.running) {
-    const int st = server_launch(ctx, d);
-    if (st) return st;
-  }
+  if (!S.running && server_launch(ctx, d)) return server_unavailable(ctx);
   // Completion is the result itself: c is set to a word no product can hold (the server's
   // q < 2^31, so 0xFFFFFFFF) before go, and the request is done when no word of c still holds it.
   // Every 4-byte store of the kernel lands whole, so this needs no release fence and no done word
@@ -704,6 +736,7 @@ int run_host(nttmul_ctx *ctx, int op, void *c, const void *a, const void *b, siz
     const int st = run_server(ctx, c, a, b, batch);
     if (st <= 0) return st;
   }
+  if (const int st = server_quiesce(ctx)) return st;
   DeviceGuard guard;
   HostJob J;
   J.op = op;
@@ -781,9 +814,18 @@ void nttmul_host_free(void *p) {
   if (p) (void)hipHostFree(p);
 }
 
-int nttmul_create_ex(nttmul_ctx **out, const nttmul_params *prm) {
-  if (!out || !prm) return NTTMUL_EINVAL;
+// The struct's size is the caller's (advisor r4): a binary built against the round 1-3 header
+// passes the six-field layout, whose knobs then take their defaults instead of being read from
+// memory past the caller's struct.
+int nttmul_create_sized(nttmul_ctx **out, const nttmul_params *caller, size_t size) {
+  if (!out) return NTTMUL_EINVAL;
   *out = nullptr;
+  if (!caller || size < NTTMUL_PARAMS_BASE_SIZE || size > sizeof(nttmul_params))
+    return NTTMUL_EINVAL;
+  nttmul_params p;
+  memset(&p, 0, sizeof(p));
+  memcpy(&p, caller, size);
+  const nttmul_params *prm = &p;
   nttmul_ctx *ctx = new (std::nothrow) nttmul_ctx();
   if (!ctx) return NTTMUL_ENOMEM;
   int st = make_plan(prm->n, prm->q, prm->psi, &ctx->plan, (prm->flags & NTTMUL_FLAG_CYCLIC) != 0);
@@ -843,6 +885,10 @@ int nttmul_create_ex(nttmul_ctx **out, const nttmul_params *prm) {
   }
   *out = ctx;
   return NTTMUL_OK;
+}
+
+int nttmul_create_ex(nttmul_ctx **ctx, const nttmul_params *prm) {
+  return nttmul_create_sized(ctx, prm, NTTMUL_PARAMS_BASE_SIZE);
 }
 
 int nttmul_create(nttmul_ctx **ctx, uint32_t n, uint64_t q, int ndev) {
@@ -1004,6 +1050,7 @@ static int device_op(nttmul_ctx *ctx, int op, void *c, const void *a, const void
   if (!ctx || (batch && (!c || !a || (two && !b)))) return NTTMUL_EINVAL;
   DevState *d = find_dev(ctx, dev);
   if (!d) return NTTMUL_ENODEV;
+  if (const int st = server_quiesce(ctx)) return st;
   DeviceGuard guard;
   HIP_TRY(ctx, hipSetDevice(d->id));
   return run_device(ctx, *d, d->dscr, op, c, a, b, batch, word_bits, (hipStream_t)stream);
@@ -1037,6 +1084,7 @@ int nttmul_fill_random_device(nttmul_ctx *ctx, void *a, void *b, uint64_t p0, si
   if (word_bits == 32 && ctx->plan.q > 0xFFFFFFFFull) return NTTMUL_EINVAL;
   DevState *d = find_dev(ctx, dev);
   if (!d) return NTTMUL_ENODEV;
+  if (const int st = server_quiesce(ctx)) return st;
   DeviceGuard guard;
   HIP_TRY(ctx, hipSetDevice(d->id));
   HIP_TRY(ctx, launch_fill(a, b, ctx->plan.logn, ctx->plan.q, seed, p0, count, word_bits,

@@ -107,6 +107,7 @@ def _bind(lib: ctypes.CDLL) -> ctypes.CDLL:
     vp, sz, u64, u32, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
     lib.nttmul_create.argtypes = [ctypes.POINTER(vp), u32, u64, i32]
     lib.nttmul_create_ex.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(_Params)]
+    lib.nttmul_create_sized.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(_Params), sz]
     lib.nttmul_destroy.argtypes = [vp]
     lib.nttmul_destroy.restype = None
     lib.nttmul_strerror.argtypes = [i32]
@@ -283,7 +284,8 @@ class Context:
                  | (NTTMUL_FLAG_SHARE_DEVICES if share_devices else 0))
         prm = _Params(n, q, psi, ndev, first_dev, flags, issue_prio, zero_copy_kb, copy_threads,
                       scratch_mb, small_server)
-        st = self._lib.nttmul_create_ex(ctypes.byref(self._h), ctypes.byref(prm))
+        st = self._lib.nttmul_create_sized(ctypes.byref(self._h), ctypes.byref(prm),
+                                           ctypes.sizeof(prm))
         if st != NTTMUL_OK:
             raise NttmulError(st, strerror(st))
         info = Info()

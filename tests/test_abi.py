@@ -12,7 +12,8 @@ import nttmul
 def test_library_exports_every_declared_symbol():
     lib = nttmul.load_library()
     syms = nttmul.exported_symbols()
-    expected = {"nttmul_create", "nttmul_create_ex", "nttmul_destroy", "nttmul_strerror",
+    expected = {"nttmul_create", "nttmul_create_ex", "nttmul_create_sized", "nttmul_destroy",
+                "nttmul_strerror",
                 "nttmul_last_error", "nttmul_get_info", "nttmul_multiply_u32",
                 "nttmul_multiply_u64", "nttmul_multiply_batch_u32", "nttmul_multiply_batch_u64",
                 "nttmul_multiply_batch_device", "nttmul_fill_random_device", "ntt256_product1",
@@ -64,13 +65,35 @@ def test_strerror_and_invalid_params():
 @pytest.mark.parametrize("field,value", [("issue_prio", 2), ("issue_prio", -2),
                                          ("zero_copy_kb", -5), ("copy_threads", -1)])
 def test_invalid_dispatch_knobs(field, value):
-    """The nttmul_params dispatch knobs (read once by nttmul_create_ex, include/nttmul.h) are
-    range-checked before any device access: an out-of-range value is NTTMUL_EINVAL."""
+    """The nttmul_params dispatch knobs (read once by nttmul_create_sized, include/nttmul.h) are
+    range-checked before any device access: an out-of-range value is NTTMUL_EINVAL.
+    nttmul_create_ex reads only the round 1-3 fields (NTTMUL_PARAMS_BASE_SIZE bytes, advisor r4),
+    so the same struct through it never sees the knob: no EINVAL (ENODEV on a host without a
+    GPU)."""
     lib = nttmul.load_library()
     h = ctypes.c_void_p()
     p = nttmul._Params(4096, 2013265921, 0, 1, 0, 0)
     setattr(p, field, value)
-    assert lib.nttmul_create_ex(ctypes.byref(h), ctypes.byref(p)) == nttmul.NTTMUL_EINVAL
+    assert lib.nttmul_create_sized(ctypes.byref(h), ctypes.byref(p), ctypes.sizeof(p)) == \
+        nttmul.NTTMUL_EINVAL
+    if not os.path.exists("/dev/kfd"):
+        assert lib.nttmul_create_ex(ctypes.byref(h), ctypes.byref(p)) == nttmul.NTTMUL_ENODEV
+
+
+def test_params_size_checked():
+    """nttmul_create_sized takes the caller's struct size: below the round 1-3 layout (n .. flags,
+    36 bytes) or above the struct this library knows is NTTMUL_EINVAL, before any device access."""
+    lib = nttmul.load_library()
+    h = ctypes.c_void_p()
+    p = nttmul._Params(4096, 2013265921, 0, 1, 0, 0)
+    base = nttmul._Params.issue_prio.offset
+    assert base == 36
+    for size in (0, base - 4, ctypes.sizeof(p) + 4):
+        assert lib.nttmul_create_sized(ctypes.byref(h), ctypes.byref(p), size) == nttmul.NTTMUL_EINVAL
+    if not os.path.exists("/dev/kfd"):
+        for size in (base, ctypes.sizeof(p)):
+            assert lib.nttmul_create_sized(ctypes.byref(h), ctypes.byref(p), size) == \
+                nttmul.NTTMUL_ENODEV
 
 
 def test_no_environment_reads_on_the_product_path():

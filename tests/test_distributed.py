@@ -37,8 +37,11 @@ def _worker(rank, world, port, outdir):
 
     wall = bench.timed_steps(step, steps=3, warmup=1, sync=lambda: None, barrier=dist.barrier)
     wmax = bench.max_over_ranks(wall + rank, dist, torch.device("cpu"))   # rank 1 is "slowest"
+    # per-rank rows for the bench line's per-rank rates and aggregate roofline
+    rows = bench.gather_ranks([wall + rank, 0.5 + rank, float(p1 - p0)], dist)
     np.save(os.path.join(outdir, f"c{rank}.npy"), out["c"])
     np.save(os.path.join(outdir, f"t{rank}.npy"), np.array([p0, p1, wall, wmax]))
+    np.save(os.path.join(outdir, f"r{rank}.npy"), np.array(rows))
     dist.destroy_process_group()
 
 
@@ -61,3 +64,15 @@ def test_two_rank_gloo(tmp_path):
     assert t[0][1] == t[1][0] == GLOBAL // 2
     # both ranks see the same max, and it is at least rank 1's own (wall + 1)
     assert t[0][3] == t[1][3] >= t[1][2] + 1
+    # every rank gathered every rank's row, in rank order
+    rows = [np.load(tmp_path / f"r{r}.npy") for r in range(2)]
+    assert np.array_equal(rows[0], rows[1]) and rows[0].shape == (2, 3)
+    assert rows[0][1][0] == t[1][2] + 1 and rows[0][1][1] == 1.5
+    agg, per = bench.rank_summary(rows[0].tolist(), 3, 3 * N * 4, 2, float(t[0][3]))
+    assert per["rates"][1] == pytest.approx(GLOBAL // 2 * 3 / (t[1][2] + 1))
+    assert per["min"] == min(per["rates"]) and per["max"] == max(per["rates"])
+    assert per["kernel_ms"] == [0.5, 1.5]
+    # the aggregate: all ranks' bytes over the slowest rank's wall time, against 2 x 8 TB/s
+    assert agg["peak"] == 16000.0
+    assert agg["achieved"] == pytest.approx(GLOBAL * 3 * N * 4 * 3 / t[0][3] / 1e9)
+    assert agg["frac"] == pytest.approx(agg["achieved"] / 16000.0)

@@ -699,8 +699,8 @@ def test_small_server_answers_promptly(torch_cuda):
 
 
 def test_small_server_restarts(torch_cuda):
-    """The server kernel leaves after 20 ms without a request and at most 1 s after its launch;
-    the host stops and relaunches it past its own 10 ms / 0.5 s margins.  Calls across idle gaps
+    """The server kernel leaves after 1 ms without a request and at most 50 ms after its launch;
+    the host stops and relaunches it past its own 0.5 ms / 25 ms margins.  Calls across idle gaps
     and past the lifetime stay exact; a context destroyed while its server runs stops it; the
     reference-width validation (NTTMUL_FLAG_VALIDATE) is done on the host for this path."""
     import time
@@ -709,14 +709,14 @@ def test_small_server_restarts(torch_cuda):
     ctx = _ctx(n, q, psi=1002, validate=True)
     t0 = time.time()
     k = 0
-    for gap in (0, 0.005, 0.015, 0.03, 0.0, 0.06):
+    for gap in (0, 0.0003, 0.0007, 0.002, 0.0, 0.005, 0.03):
         time.sleep(gap)
         a, b = O.fill_inputs(n, q, k, 1)
         k += 1
         got = ctx.multiply(a.astype(np.uint32), b.astype(np.uint32)).astype(np.uint64)
         assert ctx.last_host_path() == 3
         assert np.array_equal(got[0], P.product_merged(a[0], b[0]))
-    while time.time() - t0 < 1.2:     # past the host's 0.5 s and the kernel's 1 s lifetime
+    while time.time() - t0 < 0.2:     # past the host's 25 ms and the kernel's 50 ms lifetime
         a, b = O.fill_inputs(n, q, k, 1)
         k += 1
         got = ctx.multiply(a.astype(np.uint32), b.astype(np.uint32)).astype(np.uint64)
@@ -730,6 +730,62 @@ def test_small_server_restarts(torch_cuda):
     ctx2 = _ctx(n, q, psi=1002)
     got = ctx2.multiply(a.astype(np.uint32), b.astype(np.uint32)).astype(np.uint64)
     assert np.array_equal(got[0], P.product_merged(a[0], b[0]))
+
+
+def test_small_server_yields_to_other_work(torch_cuda):
+    """Advisor r4: a resident server kernel holds its hardware queue, so work that lands in that
+    queue waits until the kernel leaves.  The context stops its own server before it enqueues
+    anything else, and the kernel leaves 1 ms after its last request, so (1) a device-API product
+    of the same context, (2) a torch kernel and synchronize on the default stream and (3) another
+    context's server call from another thread, each issued right after a server call, finish far
+    below the old 20 ms idle window -- and every result stays exact."""
+    import threading
+    import time
+    torch = torch_cuda
+    n, q = 256, Q31
+    P = O.Plan(n, q)
+    ctx = _ctx(n, q)
+    a, b = O.fill_inputs(n, q, 31, 1)
+    a, b = a.astype(np.uint32), b.astype(np.uint32)
+    exp = P.product_merged(a[0].astype(np.uint64), b[0].astype(np.uint64))
+    da = torch.from_numpy(a.view(np.int32).ravel()).cuda()
+    db = torch.from_numpy(b.view(np.int32).ravel()).cuda()
+    dc = torch.empty_like(da)
+    s = torch.cuda.current_stream().cuda_stream
+    worst = {}
+    for it in range(10):
+        ctx.multiply(a, b)
+        assert ctx.last_host_path() == 3
+        t0 = time.perf_counter()
+        ctx.multiply_device(dc, da, db, 1, 32, stream=s)   # (1) stops the server first
+        torch.cuda.synchronize()
+        worst["device_api"] = max(worst.get("device_api", 0), time.perf_counter() - t0)
+        assert np.array_equal(dc.cpu().numpy().view(np.uint32).astype(np.uint64), exp)
+        ctx.multiply(a, b)
+        t0 = time.perf_counter()
+        x = (da + 1).sum()                                  # (2) foreign work + device sync
+        torch.cuda.synchronize()
+        worst["torch_sync"] = max(worst.get("torch_sync", 0), time.perf_counter() - t0)
+        assert int(x) == int(da.sum()) + n
+    other = _ctx(512, q)
+    a2, b2 = O.fill_inputs(512, q, 7, 1)
+    P2 = O.Plan(512, q)
+    res = {}
+
+    def call():
+        t0 = time.perf_counter()
+        res["c"] = other.multiply(a2.astype(np.uint32), b2.astype(np.uint32))
+        res["t"] = time.perf_counter() - t0
+    other.multiply(a2.astype(np.uint32), b2.astype(np.uint32))   # its server launched once
+    for it in range(10):
+        ctx.multiply(a, b)
+        th = threading.Thread(target=call)                   # (3) another context, another thread
+        th.start()
+        th.join()
+        worst["other_context"] = max(worst.get("other_context", 0), res["t"])
+        assert np.array_equal(res["c"][0].astype(np.uint64), P2.product_merged(a2[0], b2[0]))
+        assert other.last_host_path() == 3
+    assert all(t < 5e-3 for t in worst.values()), {k: f"{v * 1e3:.2f} ms" for k, v in worst.items()}
 
 
 @pytest.mark.parametrize("n,q,batch", [(4096, Q31, 1537), (256, Q30, 20000), (1024, Q62, 1100),
@@ -846,11 +902,13 @@ def test_transform_modes_device(torch_cuda):
 @pytest.mark.parametrize("world,batch", [(2, 4096), (8, 1024)])
 def test_bench_ranks_on_one_gpu(world, batch, tmp_path, torch_cuda):
     """bench.py's N > 1 path as the driver launches it (torch.distributed.run, one process per
-    rank, gloo control plane: barrier + all_reduce(MAX)), with every rank on this box's GPU(s):
-    2 ranks, and the 8-rank SCALE run's control plane (--gpus 8, 1024 products per rank).  The
-    JSON line reports n_gpus and the global batch, and the products each rank dumps from its own
-    contiguous slice [k batch, (k + 1) batch) equal the oracle's at their global
-    counter positions."""
+    rank, gloo control plane: barrier + all_reduce(MAX) + all_gather), with every rank on this
+    box's GPU(s): 2 ranks, and the 8-rank SCALE run's control plane (--gpus 8, 1024 products per
+    rank).  The JSON line reports n_gpus and the global batch, one rate per rank, the aggregate
+    roofline (all ranks' bytes over the max-over-ranks wall time against N x 8 TB/s) and rank 0's
+    CPU baseline with its cores (run after the final barrier at every N, verdict r4 item 2); the
+    products each rank dumps from its own contiguous slice [k batch, (k + 1) batch)
+    equal the oracle's at their global counter positions."""
     import socket
     import subprocess
     import sys
@@ -863,7 +921,7 @@ def test_bench_ranks_on_one_gpu(world, batch, tmp_path, torch_cuda):
         [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
          str(world), "--master-addr", "127.0.0.1", "--master-port", str(port),
          os.path.join(root, "bench.py"), "--gpus", str(world), "--steps", "3", "--warmup", "1",
-         "--settle-ms", "20", "--no-cpu-baseline", "--batch-per-gpu", str(batch),
+         "--settle-ms", "20", "--cpu-seconds", "0.5", "--batch-per-gpu", str(batch),
          "--dump-samples", prefix],
         capture_output=True, text=True, timeout=300, cwd=root)
     assert out.returncode == 0, out.stderr[-3000:]
@@ -871,6 +929,18 @@ def test_bench_ranks_on_one_gpu(world, batch, tmp_path, torch_cuda):
     assert line["n_gpus"] == world and line["config"]["global_batch"] == world * batch
     assert line["config"]["batch_per_gpu"] == batch and line["value"] > 0
     assert line["scaling"] == "weak"
+    ranks = line["ranks"]
+    assert len(ranks["rates"]) == world and all(r > 0 for r in ranks["rates"])
+    assert ranks["min"] == min(ranks["rates"]) and ranks["max"] == max(ranks["rates"])
+    assert len(ranks["kernel_ms"]) == world
+    agg = line["roofline"]["aggregate"]
+    assert agg["peak"] == 8000.0 * world
+    # value = global batch per max-over-ranks wall time, so the aggregate is the same quantity
+    assert agg["achieved"] == pytest.approx(line["value"] * 3 * 4096 * 4 / 1e9, rel=1e-9)
+    assert 0 < agg["frac"] < 1
+    cpu = line["cpu_baseline"]
+    assert cpu and cpu["value"] > 0 and cpu["cores"] >= 1 and cpu["kind"] == "port"
+    assert cpu["host_cores"]["threads"] == cpu["cores"] and f"of {world}" in cpu["note"]
     P = O.Plan(4096, Q31)
     for r in range(world):
         d = np.load(f"{prefix}.rank{r}.npz")

@@ -4,11 +4,12 @@
 //   KB_ABL_NOLOAD=1   k_rows synthesises its inputs (no global loads)
 //   KB_ABL_NOSTORE=1  k_rows folds its outputs into one conditional store (no stores)
 //   KB_ABL_NOXCHG=1   no LDS exchanges
-//   KB_ABL_L2LOAD=W   k_rows unit u reads unit u mod W (W units: L2- or Infinity-Cache-resident)
-//   KB_ABL_STROWS=W   k_rows unit u stores into unit u mod W
+//   KB_ABL_L2LOAD=W   k_rows unit u reads unit u mod W (W units: L2- or Infinity-Cache-resident;
+//                     with the tiled square split, W a multiple of 256 rows = whole polynomials)
+//   KB_ABL_STROWS=W   k_rows unit u stores into unit W + u mod W (a window apart from the loads')
 //   KB_ABL_L2CF=W     forward column pass: polynomial p reads polynomial p mod W (these are a, b)
 //   KB_ABL_L2CI=W     inverse column pass: polynomial p reads polynomial p mod W
-//   KB_ABL_STCF=W     forward column pass: polynomial p stores into polynomial p mod W
+//   KB_ABL_STCF=W     forward column pass: polynomial p stores into polynomial W + p mod W
 // Each is an NTTMUL_HOOK_* definition (the identity in the library, kernels_dev.hpp).
 #if KB_ABL_NOLOAD
 #define NTTMUL_HOOK_ROWS_INPUT(x, y, u, j)        \
@@ -32,23 +33,25 @@
 #define NTTMUL_HOOK_XCHG() return
 #endif
 #ifdef KB_ABL_L2LOAD
-#define NTTMUL_HOOK_ROWS_LD(base, u, N, b0) ((size_t)((u) % (KB_ABL_L2LOAD)) * (N) + (b0))
+#define NTTMUL_HOOK_ROWS_LD(base, u, N, b0) ((base) - (size_t)((u) - (u) % (KB_ABL_L2LOAD)) * (N))
 #endif
 #ifdef KB_ABL_STROWS
-#define NTTMUL_HOOK_ROWS_ST(base, u, N, b0) ((size_t)((u) % (KB_ABL_STROWS)) * (N) + (b0))
+#define NTTMUL_HOOK_ROWS_ST(base, u, N, b0) \
+  ((base) - (size_t)((u) - (u) % (KB_ABL_STROWS) - (KB_ABL_STROWS)) * (N))
 #endif
 #if defined(KB_ABL_L2CF) && defined(KB_ABL_L2CI)
 #define NTTMUL_HOOK_COLS_LD(base, p, sh, col, dir) \
-  ((((p) % ((dir) == 0 ? (KB_ABL_L2CF) : (KB_ABL_L2CI))) << (sh)) + (col))
+  ((base) - ((size_t)((p) - (p) % ((dir) == 0 ? (KB_ABL_L2CF) : (KB_ABL_L2CI))) << (sh)))
 #elif defined(KB_ABL_L2CF)
 #define NTTMUL_HOOK_COLS_LD(base, p, sh, col, dir) \
-  ((dir) == 0 ? ((((p) % (KB_ABL_L2CF)) << (sh)) + (col)) : (base))
+  ((dir) == 0 ? (base) - ((size_t)((p) - (p) % (KB_ABL_L2CF)) << (sh)) : (base))
 #elif defined(KB_ABL_L2CI)
 #define NTTMUL_HOOK_COLS_LD(base, p, sh, col, dir) \
-  ((dir) == 1 ? ((((p) % (KB_ABL_L2CI)) << (sh)) + (col)) : (base))
+  ((dir) == 1 ? (base) - ((size_t)((p) - (p) % (KB_ABL_L2CI)) << (sh)) : (base))
 #endif
 #ifdef KB_ABL_STCF
-#define NTTMUL_HOOK_COLS_ST(base, p, sh, col) ((((p) % (KB_ABL_STCF)) << (sh)) + (col))
+#define NTTMUL_HOOK_COLS_ST(base, p, sh, col) \
+  ((base) - ((size_t)((p) - (p) % (KB_ABL_STCF) - (KB_ABL_STCF)) << (sh)))
 #endif
 #ifndef KB_SET
 #define KB_SET 1
@@ -530,6 +533,35 @@ static hipError_t multipass_l1(const LaunchTables &T, const Conf &C, const void 
   return e;
 }
 
+// The library's square split (kernels.hip multipass_sq, NTTMUL_C5_SQ): k_cols8 forward, the row
+// pass of 256-coefficient rows, k_cols8 inverse; phases and row-pass LDS as multipass_l1
+template <class A, class IO>
+static hipError_t multipass_sq(const LaunchTables &T, const Conf &C, const void *a, const void *b,
+                               void *c, size_t batch, void *ta, void *tb, void *tc, hipStream_t s) {
+  using W = typename A::word;
+  const KParams<A> P = product_params<A>(T);
+  const size_t groups = batch * 16;
+  hipError_t e = hipSuccess;
+  if (C.mp_phase < 0 || C.mp_phase == 0) {
+    hipLaunchKernelGGL((k_cols8<A, IO, W, 0>), dim3((unsigned)groups), dim3(256), 0, s, P,
+                       (const IO *)a, (const IO *)b, (W *)ta, (W *)tb, groups);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  if (C.mp_phase < 0 || C.mp_phase == 1) {
+    const size_t units = batch << 8, blocks = (units + 15) / 16;
+    hipLaunchKernelGGL((k_rows<A, W, W, 8, 8>), dim3((unsigned)blocks), dim3(256),
+                       (unsigned)C.rows_lds_extra, s, P, (const W *)ta, (const W *)tb, (W *)tc,
+                       units);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  if (C.mp_phase < 0 || C.mp_phase == 2) {
+    hipLaunchKernelGGL((k_cols8<A, W, IO, 1>), dim3((unsigned)groups), dim3(256), 0, s, P,
+                       (const W *)tc, (const W *)nullptr, (IO *)c, (IO *)nullptr, groups);
+    e = hipGetLastError();
+  }
+  return e;
+}
+
 // The same product in one persistent launch (k_mp_persist).  scr[3]: the ticket / counter words,
 // mp_sync_bytes(batch), zeroed here on the stream before the launch.
 template <class A, class IO, int L1>
@@ -569,6 +601,8 @@ hipError_t launch(const LaunchTables &T, const Conf &C, const void *a, const voi
   if (T.word_bits != 64 || T.logn != 16 || io_bits != 64) return hipErrorNotSupported;
   if (C.mp_lag > 0 && scr[3])
     return multipass_persist<Arith64, uint64_t, 4>(T, C, a, b, c, batch, scr, s);
+  if (NTTMUL_C5_SQ)
+    return multipass_sq<Arith64, uint64_t>(T, C, a, b, c, batch, scr[0], scr[1], scr[2], s);
   return multipass_l1<Arith64, uint64_t, 4>(T, C, a, b, c, batch, scr[0], scr[1], scr[2], s);
 #else  // u32 words, q < 2^31, n <= 4096
   if (T.word_bits != 32 || T.q >= (1ull << 31) || T.logn > 12 || io_bits != 32)

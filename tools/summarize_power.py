@@ -37,9 +37,10 @@ def main():
     src, dst = sys.argv[1], sys.argv[2]
     os.makedirs(dst, exist_ok=True)
     samples, summary = {}, {}
-    static = json.load(open(os.path.join(src, "static.json")))
-    lim = static["gpu_data"][0]["limit"]["ppt0"]["socket_power_limit"]
-    summary["socket_power_limit_w"] = val(lim)
+    if os.path.exists(os.path.join(src, "static.json")):  # (tools/gpu_power.sh records it)
+        static = json.load(open(os.path.join(src, "static.json")))
+        lim = static["gpu_data"][0]["limit"]["ppt0"]["socket_power_limit"]
+        summary["socket_power_limit_w"] = val(lim)
     for f in sorted(glob.glob(os.path.join(src, "*.smi.jsonl"))):
         label = os.path.basename(f)[: -len(".smi.jsonl")]
         rows = []
