@@ -12,7 +12,7 @@ rc=$?; tail -5 $OUT/gpu_tests.txt
 case $rc in 124|134|137|139) echo "tests died rc=$rc"; exit $rc;; esac
 K=tools/kbench/bin; Q=4611686018425815041
 for i in 1 2; do
-  for v in t_base u_base o_base t_st t_ld t_ldst t_all o_st o_ld o_ldst o_all; do
+  for v in t_base u_base o_base t_spec t_st t_ld t_ldst t_all o_st o_ld o_ldst o_all; do
     tools/power_trace.sh $OUT/c5ab$i $v $K/kbench_$v 65536 $Q 1024 3000 || exit 1
     cat $OUT/c5ab$i/$v.out
   done
