@@ -228,9 +228,37 @@ static hipError_t xform_multipass_l1(const LaunchTables &T, const void *in, void
   return hipGetLastError();
 }
 
+// Standalone transforms of the square split (64-bit words at n = 65536, NTTMUL_C5_SQ, as the
+// product): forward = k_cols8 on one polynomial (tiled scratch) + the 256-coefficient row pass
+// (k_xform<..., 8, 8, 0>); inverse = the row pass into the tiled scratch + k_cols8 inverse.
+template <class A, class IO, int DIR>
+static hipError_t xform_sq(const LaunchTables &T, const void *in, void *out, size_t batch,
+                           void **scr, hipStream_t s) {
+  using W = typename A::word;
+  const size_t groups = batch * 16;
+  if (groups == 0) return hipSuccess;
+  if (DIR == 0) {
+    const KParams<A> P = make_params<A>(T);
+    hipLaunchKernelGGL((k_cols8<A, IO, W, 0, 1>), dim3((unsigned)groups), dim3(256), 0, s, P,
+                       (const IO *)in, (const IO *)nullptr, (W *)scr[0], (W *)nullptr, groups);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return launch_xform_rows<A, W, IO, 8, 8, 0>(P, scr[0], out, batch << 8, s);
+  }
+  const KParams<A> P = inverse_params<A>(T);
+  hipError_t e = launch_xform_rows<A, IO, W, 8, 8, 1>(P, in, scr[0], batch << 8, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((k_cols8<A, W, IO, 1>), dim3((unsigned)groups), dim3(256), 0, s, P,
+                     (const W *)scr[0], (const W *)nullptr, (IO *)out, (IO *)nullptr, groups);
+  return hipGetLastError();
+}
+
 template <class A, class IO, int DIR>
 static hipError_t xform_any(const LaunchTables &T, const void *in, void *out, size_t batch,
                             void **scr, hipStream_t s) {
+  if constexpr (sizeof(typename A::word) == 8 && NTTMUL_C5_SQ) {
+    if (T.logn == 16) return xform_sq<A, IO, DIR>(T, in, out, batch, scr, s);
+  }
   switch (T.logn) {
     case 13: return xform_multipass_l1<A, IO, 1, DIR>(T, in, out, batch, scr, s);
     case 14: return xform_multipass_l1<A, IO, 2, DIR>(T, in, out, batch, scr, s);

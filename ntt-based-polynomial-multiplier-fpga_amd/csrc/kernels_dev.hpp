@@ -1262,12 +1262,21 @@ __global__ __launch_bounds__(256) void k_xform(KParams<A> P, const TIn *__restri
   const size_t u = ((size_t)blockIdx.x * PB + pb) * UPG;
   const bool live = u < units, live2 = UPG == 2 && u + 1 < units;
   const int row = L1 ? (int)(u & ((1u << L1) - 1)) : 0;
-  const size_t base_in = (live ? u : 0) * N + Gr::base(GIN, j);
+  // the square split's tiled intermediate (c8_tile, as k_rows): the forward row pass reads it,
+  // the inverse row pass writes it
+  constexpr bool kTile = c8_tile(LOGS, L1);
+  constexpr int kRS = kTile ? 256 : 1;
+  static_assert(!kTile || UPG == 1, "one polynomial per thread group on the tiled layout");
+  const auto tbase = [&](size_t v, int g) {
+    return kTile ? ((v >> 8) << 16) + ((v & 255) << 4) + Gr::base(g, j) : v * N + Gr::base(g, j);
+  };
+  const size_t base_in = DIR == 0 ? tbase(live ? u : 0, GIN) : (live ? u : 0) * N + Gr::base(GIN, j);
   const size_t base_in2 = (live2 ? u + 1 : live ? u : 0) * N + Gr::base(GIN, j);
+  constexpr int kRSI = DIR == 0 ? kRS : 1, kRSO = DIR == 1 ? kRS : 1;
   W x[16], y[16];
 #pragma unroll
   for (int k = 0; k < 16; k++) {
-    x[k] = to_word<W>(in[base_in + Gr::off(GIN, k)]);
+    x[k] = to_word<W>(in[base_in + Gr::off(GIN, k) * kRSI]);
     if (UPG == 2) y[k] = to_word<W>(in[base_in2 + Gr::off(GIN, k)]);
   }
   TwPair<W> zw[16];
@@ -1276,12 +1285,12 @@ __global__ __launch_bounds__(256) void k_xform(KParams<A> P, const TIn *__restri
   else
     inv_all<A, LOGS, G - 1, L1 == 0, 0, 0, UPG>(P, x, y, lds[pb][0], lds[pb][UPG - 1], P.iw, j, row, L1);
   if (live) {
-    const size_t base_out = u * N + Gr::base(GOUT, j);
+    const size_t base_out = DIR == 1 ? tbase(u, GOUT) : u * N + Gr::base(GOUT, j);
 #pragma unroll
     for (int k = 0; k < 16; k++) {
       W v = x[k];
       if (DIR == 0 || (L1 == 0 && !A::kInvCanonical)) v = P.ar.canon(v);
-      out[base_out + Gr::off(GOUT, k)] = (TOut)v;
+      out[base_out + Gr::off(GOUT, k) * kRSO] = (TOut)v;
     }
   }
   if (live2) {
@@ -1398,13 +1407,15 @@ __global__ __launch_bounds__(256) void k_cols_inv(KParams<A> P,
 //   DIR 0: global stages 0..7 of the forward CT on a and b (twiddles P.fw[1 .. 255], uniform over
 //          the columns); X of stage 0 canonical by contract; output lazy, in place of the column
 //   DIR 1: global stages 7..0 of the inverse GS with F folded into stage 0; canonical output
-template <class A, class TIn, class TOut, int DIR>
+// NPOLY: polynomials per column group (2: a and b of a product; 1: a standalone forward transform)
+template <class A, class TIn, class TOut, int DIR, int NPOLY = DIR == 0 ? 2 : 1>
 __global__ __launch_bounds__(256) void k_cols8(KParams<A> P, const TIn *__restrict__ a,
                                                const TIn *__restrict__ b, TOut *__restrict__ ta,
                                                TOut *__restrict__ tb, size_t groups) {
   using W = typename A::word;
   using Gr = Groups<8>;
-  constexpr int CW = 16, G = Gr::G, NPOLY = DIR == 0 ? 2 : 1;
+  constexpr int CW = 16, G = Gr::G;
+  static_assert(DIR == 0 || NPOLY == 1, "the inverse column pass runs on c alone");
   constexpr int GIN = DIR == 0 ? 0 : G - 1, GOUT = DIR == 0 ? G - 1 : 0;
   static_assert(G == 2 && Gr::NP * CW >= (Gr::padx<0>(255) + 1) * CW, "Groups<8> layout");
   __shared__ W lds[Gr::NP * CW];
@@ -1428,13 +1439,13 @@ __global__ __launch_bounds__(256) void k_cols8(KParams<A> P, const TIn *__restri
   }
   if constexpr (DIR == 0) {
     TwPair<W> zw[16];
-    fwd_all<A, 8, 0, 2, 0, 0, CW>(P.ar, x, y, lds + cl, lds + cl, P.fw, jj, 0, 0, zw);
+    fwd_all<A, 8, 0, NPOLY, 0, 0, CW>(P.ar, x, y, lds + cl, lds + cl, P.fw, jj, 0, 0, zw);
     const size_t base_w = NTTMUL_HOOK_COLS_ST(ibase, p, 16, ((g & 15) << 4) + cl);
 #pragma unroll
     for (int k = 0; k < 16; k++) {
       const size_t o = (size_t)(Gr::base(GOUT, jj) + Gr::off(GOUT, k)) << kIS;
       st_stream<NTTMUL_NT_COLS>(ta + base_w + o, (TOut)x[k]);
-      st_stream<NTTMUL_NT_COLS>(tb + base_w + o, (TOut)y[k]);
+      if (NPOLY == 2) st_stream<NTTMUL_NT_COLS>(tb + base_w + o, (TOut)y[k]);
     }
   } else {
     inv_all<A, 8, G - 1, true, 0, 0, 1, CW>(P, x, y, lds + cl, lds + cl, P.iw, jj, 0, 0);

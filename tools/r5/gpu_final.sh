@@ -12,6 +12,8 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smok
 tail -1 $OUT/smoke.log
 bash tools/gpu_prof.sh $TAG c3 c5 c2 c2s 2> $OUT/prof.log || { tail -30 $OUT/prof.log; exit 1; }
 tail -5 $OUT/prof.log
+bash tools/r4/gpu_ops.sh $TAG/ops > $OUT/ops.log 2>&1 || { tail -20 $OUT/ops.log; exit 1; }
+grep " M " $OUT/ops.log
 timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/driver_cmd.json 2> $OUT/driver_cmd.err || { tail -20 $OUT/driver_cmd.err; exit 1; }
 tail -c 600 $OUT/driver_cmd.json
 timeout -k 10 300 python3 tools/r5/server_vs_ref.py > $OUT/server_vs_ref.json 2> $OUT/server_vs_ref.err || { tail -20 $OUT/server_vs_ref.err; exit 1; }
