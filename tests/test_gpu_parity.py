@@ -192,6 +192,14 @@ def test_multipass_vs_oracle(n, q, torch_cuda):
     P = O.Plan(n, q)
     ctx = _ctx(n, q, validate=True)
     assert ctx.info.kernel == 2
+    # 64-bit words at n = 65536 take the square 256 x 256 split (k_cols8, tiled intermediates),
+    # every other multi-pass product the 2^L1 x 4096 split
+    wb = 32 if q < (1 << 32) else 64
+    if n == 65536 and wb == 64:
+        assert ctx.kernel_name(64) == ("k_cols8<Arith64,u64,fwd> + k_rows<Arith64,u64,u64,8,8>"
+                                       " + k_cols8<Arith64,u64,inv>")
+    else:
+        assert ctx.kernel_name(wb).startswith("k_cols_fwd<")
     for batch in ((3, 17) if n == 8192 else (3,)):
         a, b = O.fill_inputs(n, q, 7 + batch, batch)
         a[1] = q - 1

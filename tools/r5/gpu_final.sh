@@ -18,6 +18,8 @@ if [ "$PART" = 1 ]; then
   bash tools/gpu_prof.sh $TAG c3 c5 2> $OUT/prof.log || { tail -30 $OUT/prof.log; exit 1; }
   tail -5 $OUT/prof.log
 else
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "multipass_vs_oracle or small_server" > $OUT/gpu_tests2.log 2>&1 || { tail -60 $OUT/gpu_tests2.log; exit 1; }
+  tail -1 $OUT/gpu_tests2.log
   bash tools/gpu_prof.sh $TAG c2 c2s 2> $OUT/prof2.log || { tail -30 $OUT/prof2.log; exit 1; }
   tail -5 $OUT/prof2.log
   bash tools/r4/gpu_ops.sh $TAG/ops > $OUT/ops.log 2>&1 || { tail -20 $OUT/ops.log; exit 1; }

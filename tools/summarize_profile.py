@@ -27,8 +27,18 @@ for root, _, files in os.walk(os.path.join(src, "pmc")):
     for f in files:
         if not f.endswith("_counter_collection.csv"):
             continue
-        for r in csv.DictReader(open(os.path.join(root, f))):
+        rows = sorted(csv.DictReader(open(os.path.join(root, f))), key=lambda r: int(r["Dispatch_Id"]))
+        # kernels that share a truncated name (the square split's k_cols8 forward and inverse)
+        # are told apart by their kernel id, numbered in order of first dispatch (the same order
+        # in every pass: each pass runs the same program); the ids themselves differ per pass
+        ids = collections.defaultdict(list)
+        for r in rows:
+            if r["Kernel_Id"] not in ids[r["Kernel_Name"]]:
+                ids[r["Kernel_Name"]].append(r["Kernel_Id"])
+        for r in rows:
             k = r["Kernel_Name"]
+            if len(ids[k]) > 1:
+                k = f"{k}#{ids[k].index(r['Kernel_Id'])}"
             pmc[(k, r["Counter_Name"])].append(float(r["Counter_Value"]))
             dur[k].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 out = {}
