@@ -153,3 +153,27 @@ def test_product_sources_hold_no_kbench_code():
         for banned in ("NTTMUL_KBENCH", "NTTMUL_ABL_", "k_mp_persist", "k_rows_w4", "k_rows_pipe",
                        "k_rows_ab", "mp_lag", "pipe_per_wave", "rows_lds_extra"):
             assert banned not in text, (name, banned)
+
+
+@pytest.mark.parametrize("flags", [
+    ["-DKB_SET=1"],
+    ["-DKB_SET=1", "-DKB_ABL_NOLOAD=1", "-DKB_ABL_NOSTORE=1", "-DKB_ABL_NOXCHG=1"],
+    ["-DKB_SET=1", "-DKB_ABL_L2LOAD=64"],
+    ["-DKB_SET=2"],
+    ["-DKB_SET=2", "-DNTTMUL_C5_SQ=0", "-DKB_ABL_STROWS=16", "-DKB_ABL_STCF=1"],
+    ["-DKB_SET=2", "-DKB_ABL_STROWS=256", "-DKB_ABL_STCF=1", "-DKB_ABL_L2LOAD=256",
+     "-DKB_ABL_L2CI=1", "-DKB_ABL_L2CF=1"],
+    ["-DKB_SET=2", "-DKB_ABL_L2CI=1"]])
+def test_kbench_sources_compile(flags):
+    """tools/kbench compiles the library's device code (csrc/kernels_dev.hpp) with its own
+    launchers and pricing hooks: every kernel set and hook combination it is built with stays a
+    valid translation unit (semantic check of every instantiated template, no code generation)."""
+    root = os.path.dirname(nttmul.PKG_DIR)
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-std=c++17", "-fsyntax-only",
+           "-I" + os.path.join(root, "include"), "-I" + os.path.join(nttmul.PKG_DIR, "csrc"),
+           "-I" + os.path.join(root, "tools", "kbench"), *flags,
+           os.path.join(root, "tools", "kbench", "kb_kernels.hip")]
+    if not os.path.exists(cmd[0]):
+        pytest.skip("hipcc not present")
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
