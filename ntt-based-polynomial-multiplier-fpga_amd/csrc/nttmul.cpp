@@ -904,7 +904,7 @@ void nttmul_destroy(nttmul_ctx *ctx) {
   if (!ctx) return;
   DeviceGuard guard;
   Server &S = ctx->server;
-  if (S.box || S.req) {
+  if (S.box || S.req || S.s) {  // whatever a partial server_alloc left behind
     (void)hipSetDevice(ctx->dev[0].id);
     (void)server_stop(ctx);
     if (S.s) (void)hipStreamDestroy(S.s);
