@@ -90,6 +90,8 @@
 //   NTTMUL_HOOK_ROWS_INPUT(x, y, u, j)      k_rows: statement after the loads (may overwrite x, y)
 //   NTTMUL_HOOK_ROWS_OUTPUT(x, c, base, live) k_rows: statement before the stores (may return)
 //   NTTMUL_HOOK_XCHG()                      exchange: statement before the LDS round trip
+//   NTTMUL_HOOK_TW(tw, idx, dir)            transform stages (untyped twiddle tables; dir 0
+//                                           forward, 1 inverse): the pair tw[idx]
 //   NTTMUL_HOOK_COLS_LD(base, p, sh, col, dir) column passes (dir 0 forward, 1 inverse): word
 //                                           offset their loads start from
 //   NTTMUL_HOOK_COLS_ST(base, p, sh, col)   column passes: word offset of the intermediates' stores
@@ -104,6 +106,9 @@
 #endif
 #ifndef NTTMUL_HOOK_ROWS_OUTPUT
 #define NTTMUL_HOOK_ROWS_OUTPUT(x, c, base, live) do { } while (0)
+#endif
+#ifndef NTTMUL_HOOK_TW
+#define NTTMUL_HOOK_TW(tw, idx, dir) ((tw)[idx])
 #endif
 #ifndef NTTMUL_HOOK_XCHG
 #define NTTMUL_HOOK_XCHG() do { } while (0)
@@ -365,7 +370,7 @@ __device__ __forceinline__ void fwd_stage(const A &ar, typename A::word (&x)[16]
 #undef NTTMUL_CT_T
       continue;
     }
-    const TwPair<typename A::word> t = tw[idx];
+    const TwPair<typename A::word> t = NTTMUL_HOOK_TW(tw, idx, 0);
     if (l == S - SKIP - 1) zw[k] = t;
     if constexpr (kTypedP<A>()) {
       // Arith32P: register k was written as a (signed) difference by the previous stage iff
@@ -489,7 +494,7 @@ __device__ __forceinline__ void inv_stage(const KParams<A> &P, typename A::word 
     } else {
       const int m = k / ns;
       const int idx = tbase + (Gr::blk(g, j, k) << l) + (m >> (S - l));
-      const TwPair<typename A::word> t = tw[idx];
+      const TwPair<typename A::word> t = NTTMUL_HOOK_TW(tw, idx, 1);
       P.ar.gs(x[k], x[k + dist], t.w, t.ws);
     }
   }

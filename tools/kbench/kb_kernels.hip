@@ -53,6 +53,44 @@
 #define NTTMUL_HOOK_COLS_ST(base, p, sh, col) \
   ((base) - ((size_t)((p) - (p) % (KB_ABL_STCF) - (KB_ABL_STCF)) << (sh)))
 #endif
+#include <hip/hip_runtime.h>
+#include <type_traits>
+// twiddle pairs of the transform stages (KB_SET 1's products):
+//   KB_ABL_NOTW=1     synthesised from the table index in registers (no twiddle loads; one
+//                     multiply per pair in their place; wrong results)
+//   KB_TW_LDS=1       k_rows copies the forward and inverse pairs 0..511 (every pair a 4096-point
+//                     product with 8-coefficient base blocks uses) into LDS once per workgroup and
+//                     reads them there (exact for n <= 4096 with D = 3; other shapes not)
+#if KB_ABL_NOTW
+template <class T>
+__device__ __forceinline__ T kb_notw(int idx) {
+  using W = decltype(T::w);
+  return T{(W)((uint32_t)idx * 0x9E3779B1u), (W)(uint32_t)idx};
+}
+#define NTTMUL_HOOK_TW(tw, idx, dir) kb_notw<std::remove_cv_t<std::remove_reference_t<decltype(*(tw))>>>(idx)
+#endif
+#if KB_TW_LDS
+__shared__ uint2 kb_tws[2][512];
+template <class T>
+__device__ __forceinline__ void kb_stage_tw(const T *fw, const T *iw) {
+  static_assert(sizeof(T) == 8, "u32 pairs");
+  const uint4 *f4 = (const uint4 *)fw, *i4 = (const uint4 *)iw;
+  uint4 *l4 = (uint4 *)&kb_tws[0][0];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) {  // 2 x 512 pairs = 512 uint4
+    l4[i] = f4[i];
+    l4[256 + i] = i4[i];
+  }
+  __syncthreads();
+}
+template <class T>
+__device__ __forceinline__ T kb_tw_lds(int idx, int dir) {
+  const uint2 v = kb_tws[dir][idx & 511];
+  return T{v.x, v.y};
+}
+#define NTTMUL_HOOK_ROWS_INPUT(x, y, u, j) kb_stage_tw(P.fw, P.iw)
+#define NTTMUL_HOOK_TW(tw, idx, dir) \
+  kb_tw_lds<std::remove_cv_t<std::remove_reference_t<decltype(*(tw))>>>(idx, dir)
+#endif
 #ifndef KB_SET
 #define KB_SET 1
 #endif
