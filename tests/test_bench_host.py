@@ -188,3 +188,18 @@ def test_op_defaults_to_the_product():
     assert bench.parse(["--op", "inverse"]).op == "inverse"
     with pytest.raises(SystemExit):
         bench.parse(["--op", "square"])
+
+
+def test_committed_profiles_describe_the_shipped_library():
+    """The driver's bench line reads traffic and valu_roofline from the committed profiles only
+    when they were measured on this build's code object (bench.py fails closed otherwise): the
+    in-tree libnttmul.so must have a PMC entry for C3, C2 and C5 and a VALU bound for C3 / C2."""
+    if not os.path.exists(nttmul.LIB_PATH):
+        pytest.skip("libnttmul.so not built")
+    co = nttmul.code_object_id()
+    for n, q, batch in ((4096, 2013265921, 65536), (1024, 2013265921, 4096),
+                        (65536, 0x3FFFFFFFFFE80001, 1024)):
+        traffic, why = bench.load_traffic(n, q, batch, co)
+        assert traffic is not None, why
+    for n in (4096, 1024):
+        assert bench.load_valu_bound(n, 2013265921, co) is not None, f"no VALU bound of {co} at n={n}"
