@@ -4,7 +4,7 @@
 // include kernels_dev.hpp with launchers of their own and never compile this file.
 #if defined(NTTMUL_HOOK_ROWS_LD) || defined(NTTMUL_HOOK_ROWS_ST) || defined(NTTMUL_HOOK_ROWS_INPUT) || \
     defined(NTTMUL_HOOK_ROWS_OUTPUT) || defined(NTTMUL_HOOK_XCHG) || defined(NTTMUL_HOOK_COLS_LD) || \
-    defined(NTTMUL_HOOK_COLS_ST) || defined(NTTMUL_HOOK_TW)
+    defined(NTTMUL_HOOK_COLS_ST) || defined(NTTMUL_HOOK_TW) || defined(NTTMUL_HOOK_PRIO0)
 #error "NTTMUL_HOOK_* are tools/kbench instrumentation points (wrong-result pricing builds), not library switches"
 #endif
 #include "kernels_dev.hpp"

@@ -90,6 +90,8 @@
 //   NTTMUL_HOOK_ROWS_INPUT(x, y, u, j)      k_rows: statement after the loads (may overwrite x, y)
 //   NTTMUL_HOOK_ROWS_OUTPUT(x, c, base, live) k_rows: statement before the stores (may return)
 //   NTTMUL_HOOK_XCHG()                      exchange: statement before the LDS round trip
+//   NTTMUL_HOOK_PRIO0(u)                    k_rows issue-priority variant: the statement that
+//                                           sets the wave's priority before its loads
 //   NTTMUL_HOOK_TW(tw, idx, dir)            transform stages (untyped twiddle tables; dir 0
 //                                           forward, 1 inverse): the pair tw[idx]
 //   NTTMUL_HOOK_COLS_LD(base, p, sh, col, dir) column passes (dir 0 forward, 1 inverse): word
@@ -106,6 +108,9 @@
 #endif
 #ifndef NTTMUL_HOOK_ROWS_OUTPUT
 #define NTTMUL_HOOK_ROWS_OUTPUT(x, c, base, live) do { } while (0)
+#endif
+#ifndef NTTMUL_HOOK_PRIO0
+#define NTTMUL_HOOK_PRIO0(u) __builtin_amdgcn_s_setprio(3)
 #endif
 #ifndef NTTMUL_HOOK_TW
 #define NTTMUL_HOOK_TW(tw, idx, dir) ((tw)[idx])
@@ -744,7 +749,7 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
   const size_t base_r = NTTMUL_HOOK_ROWS_LD(base_l, u, N, Gr::base(0, j));
 
   CLK_STAMP(0);
-  if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);  // rows_prio
+  if constexpr (PRIO) NTTMUL_HOOK_PRIO0(u);  // rows_prio
   W x[16], y[16];
   // NTTMUL_CPOL >= 0: a, b, c of a one-product-per-block u32 product through buffer loads /
   // stores (descriptor from block-uniform values, 32-bit per-lane offsets, nt by default)

@@ -126,7 +126,8 @@ def test_no_device_host_alloc():
 @pytest.mark.parametrize("hook", ["NTTMUL_HOOK_ROWS_LD(b,u,N,b0)=0", "NTTMUL_HOOK_ROWS_ST(b,u,N,b0)=0",
                                   "NTTMUL_HOOK_ROWS_INPUT(x,y,u,j)=", "NTTMUL_HOOK_ROWS_OUTPUT(x,c,b,l)=",
                                   "NTTMUL_HOOK_XCHG()=", "NTTMUL_HOOK_COLS_LD(b,p,s,c,d)=0",
-                                  "NTTMUL_HOOK_COLS_ST(b,p,s,c)=0", "NTTMUL_HOOK_TW(t,i,d)=0"])
+                                  "NTTMUL_HOOK_COLS_ST(b,p,s,c)=0", "NTTMUL_HOOK_TW(t,i,d)=0",
+                                  "NTTMUL_HOOK_PRIO0(u)="])
 def test_instrumentation_hooks_refuse_library_build(hook):
     """The wrong-result pricing variants live in tools/kbench (kb_kernels.hip defines the
     NTTMUL_HOOK_* points of csrc/kernels_dev.hpp); the library's translation unit kernels.hip

@@ -91,6 +91,43 @@ __device__ __forceinline__ T kb_tw_lds(int idx, int dir) {
 #define NTTMUL_HOOK_TW(tw, idx, dir) \
   kb_tw_lds<std::remove_cv_t<std::remove_reference_t<decltype(*(tw))>>>(idx, dir)
 #endif
+// load order of a one-generation launch (C2: 4,096 one-wave products, 4 per SIMD, every wave's
+// data lands late because the memory system interleaves all of their loads):
+//   KB_PRIO_GEN=G     issue-priority variant only: unit u issues its loads at priority
+//                     3 - min(3, u / G) (G = the units of one generation, 1,024 at C2), then
+//                     returns to 3 once they are issued, so the first generation's loads queue
+//                     ahead of the later ones' and its arithmetic starts while theirs stream in
+//                     (exact)
+#if KB_PRIO_GEN
+__device__ __forceinline__ void kb_prio_gen(size_t u) {
+  // (the priority ladder as one asm block with its own branches: compiler-visible branches here
+  // moved the kernel's `live` select into VGPRs and wrapped every load in a waterfall loop)
+  const uint32_t g = __builtin_amdgcn_readfirstlane((uint32_t)(u / (KB_PRIO_GEN)));
+  asm volatile(
+      "s_cmp_lt_u32 %0, 1\n\t"
+      "s_cbranch_scc1 .Lkbp3_%=\n\t"
+      "s_cmp_lt_u32 %0, 2\n\t"
+      "s_cbranch_scc1 .Lkbp2_%=\n\t"
+      "s_cmp_lt_u32 %0, 3\n\t"
+      "s_cbranch_scc1 .Lkbp1_%=\n\t"
+      "s_setprio 0\n\t"
+      "s_branch .Lkbpe_%=\n"
+      ".Lkbp1_%=:\n\t"
+      "s_setprio 1\n\t"
+      "s_branch .Lkbpe_%=\n"
+      ".Lkbp2_%=:\n\t"
+      "s_setprio 2\n\t"
+      "s_branch .Lkbpe_%=\n"
+      ".Lkbp3_%=:\n\t"
+      "s_setprio 3\n"
+      ".Lkbpe_%=:"
+      :
+      : "s"(g)
+      : "scc");
+}
+#define NTTMUL_HOOK_PRIO0(u) kb_prio_gen(u)
+#define NTTMUL_HOOK_ROWS_INPUT(x, y, u, j) __builtin_amdgcn_s_setprio(3)
+#endif
 #ifndef KB_SET
 #define KB_SET 1
 #endif
@@ -633,8 +670,22 @@ static hipError_t multipass_persist(const LaunchTables &T, const Conf &C, const 
   return hipGetLastError();
 }
 
+static hipError_t launch_(const LaunchTables &T, const Conf &C, const void *a, const void *b,
+                          void *c, size_t batch, int io_bits, void **scr, hipStream_t s);
+// the library's launch_polymul rule for the issue-priority variant (kernels_dev.hpp rows_prio):
+// one-generation launches of the Plantard kernels take it (C2), unless T.prio says otherwise
 hipError_t launch(const LaunchTables &T, const Conf &C, const void *a, const void *b, void *c,
                   size_t batch, int io_bits, void **scr, hipStream_t s) {
+  const int prev = tl_prio_cus, prev_mode = tl_prio_mode;
+  tl_prio_cus = T.prio_ok ? T.cus : 0;
+  tl_prio_mode = T.prio;
+  const hipError_t e = launch_(T, C, a, b, c, batch, io_bits, scr, s);
+  tl_prio_cus = prev;
+  tl_prio_mode = prev_mode;
+  return e;
+}
+static hipError_t launch_(const LaunchTables &T, const Conf &C, const void *a, const void *b,
+                          void *c, size_t batch, int io_bits, void **scr, hipStream_t s) {
 #if KB_SET == 2  // C5: 64-bit words, n = 65536
   if (T.word_bits != 64 || T.logn != 16 || io_bits != 64) return hipErrorNotSupported;
   if (C.mp_lag > 0 && scr[3])

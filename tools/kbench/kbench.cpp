@@ -45,6 +45,8 @@ int main(int argc, char **argv) {
   T.f8 = P.f8; T.f8s = P.f8s; T.wf8 = P.wf8; T.wf8s = P.wf8s;
   T.fi = P.fi; T.fis = P.fis; T.wfi = P.wfi; T.wfis = P.wfis; T.r2 = P.r2;
   CK(hipDeviceGetAttribute(&T.cus, hipDeviceAttributeMultiprocessorCount, 0));
+  // KB_PRIO: the issue-priority variant as nttmul_params.issue_prio (-1 never, 0 automatic, 1 always)
+  T.prio = getenv("KB_PRIO") ? atoi(getenv("KB_PRIO")) : 0;
   kb::Conf C;
   // KB_MP_LAG > 0: n > 4096 products as one persistent launch (k_mp_persist) with this lag
   C.mp_lag = getenv("KB_MP_LAG") ? atoi(getenv("KB_MP_LAG")) : 0;
