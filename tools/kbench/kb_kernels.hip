@@ -128,6 +128,39 @@ __device__ __forceinline__ void kb_prio_gen(size_t u) {
 #define NTTMUL_HOOK_PRIO0(u) kb_prio_gen(u)
 #define NTTMUL_HOOK_ROWS_INPUT(x, y, u, j) __builtin_amdgcn_s_setprio(3)
 #endif
+// vector-memory instruction count of the coefficient streams (u32 products; wrong results):
+//   KB_ABL_X4LOAD=1   a and b arrive by 16-byte loads (4 per polynomial per lane instead of 16
+//                     dword loads), each lane's 16 consecutive-in-memory words landing in its
+//                     registers unpermuted (the bytes of the product, a quarter of the instructions)
+//   KB_ABL_X4STORE=1  c leaves by 16-byte stores the same way
+typedef unsigned int kb_u4 __attribute__((ext_vector_type(4)));
+#if KB_ABL_X4LOAD
+#define NTTMUL_HOOK_ROWS_INPUT(x, y, u, j)                                                   \
+  do {                                                                                      \
+    const kb_u4 *pa_ = (const kb_u4 *)(a + (live ? u : 0) * N);                             \
+    const kb_u4 *pb_ = (const kb_u4 *)(b + (live ? u : 0) * N);                             \
+    _Pragma("unroll") for (int m_ = 0; m_ < 4; m_++) {                                      \
+      const kb_u4 va_ = __builtin_nontemporal_load(pa_ + (j) + TP * m_);                    \
+      const kb_u4 vb_ = __builtin_nontemporal_load(pb_ + (j) + TP * m_);                    \
+      x[4 * m_] = va_.x; x[4 * m_ + 1] = va_.y; x[4 * m_ + 2] = va_.z; x[4 * m_ + 3] = va_.w; \
+      y[4 * m_] = vb_.x; y[4 * m_ + 1] = vb_.y; y[4 * m_ + 2] = vb_.z; y[4 * m_ + 3] = vb_.w; \
+    }                                                                                       \
+  } while (0)
+#endif
+#if KB_ABL_X4STORE
+#define NTTMUL_HOOK_ROWS_OUTPUT(x, c, base, live)                                  \
+  do {                                                                             \
+    if (live) {                                                                    \
+      kb_u4 *pc_ = (kb_u4 *)((c) + u * N);                                         \
+      _Pragma("unroll") for (int m_ = 0; m_ < 4; m_++) {                           \
+        kb_u4 v_;                                                                  \
+        v_.x = x[4 * m_]; v_.y = x[4 * m_ + 1]; v_.z = x[4 * m_ + 2]; v_.w = x[4 * m_ + 3]; \
+        __builtin_nontemporal_store(v_, pc_ + j + TP * m_);                        \
+      }                                                                            \
+    }                                                                              \
+    return;                                                                        \
+  } while (0)
+#endif
 #ifndef KB_SET
 #define KB_SET 1
 #endif
