@@ -147,6 +147,12 @@ int fail(nttmul_ctx *ctx, hipError_t e, const char *what) {
   return e == hipErrorOutOfMemory ? NTTMUL_ENOMEM : NTTMUL_EHIP;
 }
 
+// a status message of our own (same lock as fail)
+void set_err(nttmul_ctx *ctx, const char *msg) {
+  std::lock_guard<std::mutex> l(g_err_mu);
+  snprintf(ctx->err, sizeof(ctx->err), "%s", msg);
+}
+
 #define HIP_TRY(ctx, expr)                          \
   do {                                              \
     hipError_t _e = (expr);                         \
@@ -258,7 +264,7 @@ int run_device(nttmul_ctx *ctx, DevState &d, Scratch &sc, int op, void *c, const
     HIP_TRY(ctx, hipMemcpyAsync(&bad, d.flag, sizeof(int), hipMemcpyDeviceToHost, s));
     HIP_TRY(ctx, hipStreamSynchronize(s));
     if (bad) {
-      snprintf(ctx->err, sizeof(ctx->err), "input coefficient >= q");
+      set_err(ctx, "input coefficient >= q");
       return NTTMUL_ERANGE;
     }
   }
@@ -461,7 +467,7 @@ int run_host_dev(nttmul_ctx *ctx, DevState &d, const HostJob &J, size_t p0, size
 // WaitForDoneAll (NTT_PCIECommunicationv2.c:83-107, 211-215) without a kernel launch per call.
 // The caller's a, b go into the mailbox, go = seq releases them, and the host spins on done;
 // the resident kernel is (re)launched when it is not known to be alive: never launched, idle on
-// the host's clock for longer than kServerIdleHost (it leaves after 20 ms on its own), older than
+// the host's clock for longer than kServerIdleHost (it leaves after 1 ms on its own), older than
 // kServerLifeHost, or found finished while a request waits.  Every spin is bounded.
 // The go word into the request half.  A BAR mapping of device memory is uncached or
 // write-combining on the host, so the fences keep a and b ahead of go and push go out at once.
@@ -556,7 +562,7 @@ int server_unavailable(nttmul_ctx *ctx) {
   ctx->small_server = -1;
   ctx->server.running = false;
   (void)hipGetLastError();
-  ctx->err[0] = 0;
+  set_err(ctx, "");  // (the failure that led here is handled: the launch path runs)
   return 1;
 }
 
@@ -572,7 +578,7 @@ int run_server(nttmul_ctx *ctx, void *c, const void *a, const void *b, size_t ba
     const uint32_t *pa = (const uint32_t *)a, *pb = (const uint32_t *)b;
     for (size_t i = 0; i < words; i++)
       if (pa[i] >= P.q || pb[i] >= P.q) {
-        snprintf(ctx->err, sizeof(ctx->err), "input coefficient >= q");
+        set_err(ctx, "input coefficient >= q");
         return NTTMUL_ERANGE;
       }
   }
@@ -622,7 +628,7 @@ int run_server(nttmul_ctx *ctx, void *c, const void *a, const void *b, size_t ba
     }
     if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
       (void)server_stop(ctx);
-      snprintf(ctx->err, sizeof(ctx->err), "device server: no answer within 5 s");
+      set_err(ctx, "device server: no answer within 5 s");
       return NTTMUL_EHIP;
     }
   }
