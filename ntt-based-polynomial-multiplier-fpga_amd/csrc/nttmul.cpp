@@ -620,8 +620,8 @@ int run_server(nttmul_ctx *ctx, void *c, const void *a, const void *b, size_t ba
       // this request after the check above, or it left before it saw it -- then relaunch
       if (landed()) break;
       S.running = false;
-      const int st = server_launch(ctx, d);
-      if (st) return st;
+      // (a relaunch the runtime refuses: this request and every later one take the launch path)
+      if (server_launch(ctx, d)) return server_unavailable(ctx);
     } else if (q != hipErrorNotReady) {
       S.running = false;
       return fail(ctx, q, "device server");
