@@ -600,6 +600,38 @@ def test_cyclic_vs_schoolbook(n, q, torch_cuda):
         assert np.array_equal(c[i], O.cyclic_schoolbook(a[i], b[i], n, q)), (n, q, i)
 
 
+def _horner(coeffs, y, q):
+    acc = 0
+    for v in reversed([int(x) for x in coeffs]):
+        acc = (acc * y + v) % q
+    return acc
+
+
+@pytest.mark.parametrize("n,q", [(65536, Q62), (65536, Q32), (32768, Q31), (16384, Q62)])
+def test_cyclic_multipass(n, q, torch_cuda):
+    """Cyclic products (NTTMUL_FLAG_CYCLIC, the FPGA flow's x^n - 1) on the multi-pass kernels,
+    including the square split at n = 65536 with 64-bit words, where a schoolbook check is out of
+    reach: a monomial product is an exact rotation, and a random product agrees with
+    a(w^r) b(w^r) at random n-th roots of unity (c = a b mod x^n - 1 evaluates multiplicatively
+    there)."""
+    ctx = _ctx(n, q, cyclic=True)
+    assert ctx.info.cyclic == 1 and ctx.info.kernel == 2
+    omega = int(ctx.info.omega)
+    assert pow(omega, n, q) == 1 and pow(omega, n // 2, q) == q - 1
+    a, b = O.fill_inputs(n, q, 91, 3)
+    rng = np.random.default_rng(n ^ (q & 0xFFFF))
+    k = int(rng.integers(1, n - 1))
+    b[1] = 0; b[1, n - 1] = 1                       # a x^(n-1): c[j] = a[(j + 1) mod n]
+    b[2] = 0; b[2, k] = 1                           # a x^k:     c[j] = a[(j - k) mod n]
+    dt = np.uint32 if q < (1 << 32) else np.uint64
+    c = ctx.multiply(a.astype(dt), b.astype(dt)).astype(np.uint64)
+    assert np.array_equal(c[1], np.roll(a[1], -1)), (n, q)
+    assert np.array_equal(c[2], np.roll(a[2], k)), (n, q, k)
+    for r in (int(x) for x in rng.integers(1, n, 3)):
+        y = pow(omega, r, q)
+        assert _horner(c[0], y, q) == _horner(a[0], y, q) * _horner(b[0], y, q) % q, (n, q, r)
+
+
 def test_time_testing_gpu_app(golden_dir, torch_cuda):
     """apps/time_testing_gpu (time_testing256.c on the C ABI) prints the reference's product of
     the reference's own coefficient files."""
