@@ -169,6 +169,9 @@ typedef unsigned int kb_u4 __attribute__((ext_vector_type(4)));
 #include "kb.hpp"
 
 namespace nttmul {
+#if KB_PL
+#include "kb_rows_pl.inc"
+#endif
 
 // C2 in-launch overlap experiments (each measured slower than k_rows at C2 and at
 // n = 1024 x 262144, profiles/r3/c2/)
@@ -601,6 +604,27 @@ static hipError_t fused(const LaunchTables &T, const Conf &C, const void *a, con
       return hipGetLastError();
     }
   }
+#if KB_PL
+  // KB_PL: the n = 1024 product through k_rows_pl (tools/kbench/gen_rows_pl.py: the same kernel,
+  // arguments a, b, c, units first so -amdgpu-kernarg-preload-count can preload them)
+  if constexpr (IsPlantard<A>::value) {
+    if (T.logn == 10) {
+      constexpr int NT = rows_threads(10), PB = NT / 64;
+      const size_t blocks = (batch + PB - 1) / PB;
+      if (blocks == 0) return hipSuccess;
+      const bool prio = rows_prio(blocks * (NT / 64));
+      if (prio)
+        hipLaunchKernelGGL((k_rows_pl<A, uint32_t, uint32_t, 10, 0, true>), dim3((unsigned)blocks),
+                           dim3(NT), 0, s, (const uint32_t *)a, (const uint32_t *)b,
+                           (uint32_t *)c, batch, P);
+      else
+        hipLaunchKernelGGL((k_rows_pl<A, uint32_t, uint32_t, 10, 0>), dim3((unsigned)blocks),
+                           dim3(NT), 0, s, (const uint32_t *)a, (const uint32_t *)b,
+                           (uint32_t *)c, batch, P);
+      return hipGetLastError();
+    }
+  }
+#endif
   switch (T.logn) {
     case 8: return launch_rows<A, uint32_t, uint32_t, 8, 0>(P, a, b, c, batch, s);
     case 9: return launch_rows<A, uint32_t, uint32_t, 9, 0>(P, a, b, c, batch, s);
