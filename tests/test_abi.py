@@ -3,6 +3,7 @@ declares, and reports errors (never falls back to a CPU path) when no GPU is pre
 import ctypes
 import os
 import subprocess
+import sys
 
 import pytest
 
@@ -164,17 +165,24 @@ def test_product_sources_hold_no_kbench_code():
     ["-DKB_SET=2", "-DNTTMUL_C5_SQ=0", "-DKB_ABL_STROWS=16", "-DKB_ABL_STCF=1"],
     ["-DKB_SET=2", "-DKB_ABL_STROWS=256", "-DKB_ABL_STCF=1", "-DKB_ABL_L2LOAD=256",
      "-DKB_ABL_L2CI=1", "-DKB_ABL_L2CF=1"],
-    ["-DKB_SET=2", "-DKB_ABL_L2CI=1"]])
-def test_kbench_sources_compile(flags):
+    ["-DKB_SET=2", "-DKB_ABL_L2CI=1"],
+    ["-DKB_SET=1", "-DKB_ABL_NOTW=1"], ["-DKB_SET=1", "-DKB_TW_LDS=1"],
+    ["-DKB_SET=1", "-DKB_PRIO_GEN=1024"],
+    ["-DKB_SET=1", "-DKB_ABL_X4LOAD=1", "-DKB_ABL_X4STORE=1"],
+    ["-DKB_SET=1", "-DKB_PL=1"]])
+def test_kbench_sources_compile(flags, tmp_path):
     """tools/kbench compiles the library's device code (csrc/kernels_dev.hpp) with its own
     launchers and pricing hooks: every kernel set and hook combination it is built with stays a
     valid translation unit (semantic check of every instantiated template, no code generation)."""
     root = os.path.dirname(nttmul.PKG_DIR)
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-std=c++17", "-fsyntax-only",
            "-I" + os.path.join(root, "include"), "-I" + os.path.join(nttmul.PKG_DIR, "csrc"),
-           "-I" + os.path.join(root, "tools", "kbench"), *flags,
+           "-I" + os.path.join(root, "tools", "kbench"), "-I" + str(tmp_path), *flags,
            os.path.join(root, "tools", "kbench", "kb_kernels.hip")]
     if not os.path.exists(cmd[0]):
         pytest.skip("hipcc not present")
+    # (KB_PL: the reordered-argument k_rows, generated from the product source)
+    subprocess.run([sys.executable, os.path.join(root, "tools", "kbench", "gen_rows_pl.py"),
+                    str(tmp_path)], check=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-3000:]

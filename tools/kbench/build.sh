@@ -8,9 +8,11 @@ R=$(cd "$(dirname "$0")/../.." && pwd)
 P=$R/ntt-based-polynomial-multiplier-fpga_amd
 OUT=${KB_OUT:-$R/tools/kbench/bin}
 mkdir -p $OUT
+# (KB_PL=1 variants include the generated reordered-argument k_rows)
+python3 $R/tools/kbench/gen_rows_pl.py
 build() {
   local name=$1; shift
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -I$R/include -I$P/csrc -I$R/tools/kbench -DVARIANT="\"$name\"" ${KB_FLAGS:--DKB_SET=1} "$@" \
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -I$R/include -I$P/csrc -I$R/tools/kbench -I$R/tools/kbench/bin -DVARIANT="\"$name\"" ${KB_FLAGS:--DKB_SET=1} "$@" \
     $R/tools/kbench/kbench.cpp $R/tools/kbench/kb_kernels.hip $P/csrc/planner.cpp -o $OUT/kbench_$name &
 }
 if [ $# -eq 0 ]; then set -- base; fi
