@@ -127,9 +127,10 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--n", type=int, default=4096)
     ap.add_argument("--q", type=int, default=2013265921)
-    ap.add_argument("--batch-per-gpu", type=int, default=65536,
-                    help="polymults per GPU per step, the same at every N (weak scaling; default "
-                         "C3's 65536; C4 = --batch-per-gpu 131072 at 8 ranks: 2^20 in all)")
+    ap.add_argument("--batch-per-gpu", type=int, default=None,
+                    help="polymults per GPU per step (default: C3's 65536 per GPU at 1, 2 and 4 "
+                         "ranks; at 8 ranks C4's 131072, i.e. BASELINE configs[3]'s 2^20 split "
+                         "across 8 GPUs)")
     ap.add_argument("--word-bits", type=int, default=0, help="32/64 coefficient storage (0: auto)")
     ap.add_argument("--op", choices=sorted(OPS), default="multiply",
                     help="multiply (the BASELINE metric); forward / inverse / pointwise time the "
@@ -162,6 +163,20 @@ def parse(argv=None):
                     help="write <prefix>.rank<r>.npz with sampled products of this rank's slice "
                          "(checked against the oracle by tests/test_gpu_parity.py)")
     return ap.parse_args(argv)
+
+
+C3_BATCH = 65536             # BASELINE configs[2]: n = 4096, batch 65536 on one GPU
+C4_GLOBAL = 1 << 20         # BASELINE configs[3]: n = 4096, batch 2^20 split across 8 GPUs
+
+
+def default_batch(n: int, world: int) -> int:
+    """Polymults per GPU per step when --batch-per-gpu is not given: C3's 65536 on 1, 2 and 4
+    GPUs (so per-GPU work is C3's), and at 8 GPUs C4's 2^20 / 8 = 131072, so the driver's 8-GPU
+    line is BASELINE's C4 workload (one C3-sized kernel rate either way: the product kernel's
+    per-GPU throughput does not depend on the batch beyond a few generations of workgroups)."""
+    if n == 4096 and world == 8:
+        return C4_GLOBAL // 8
+    return C3_BATCH
 
 
 def cpu_baseline(n: int, q: int, target_s: float):
@@ -302,36 +317,72 @@ def host_io(ctx, a_dev, b_dev, batch: int, n: int, wb: int, reps: int = 3):
     return line
 
 
-def _profile_entry(name: str, n: int, q: int, code_object: str):
-    """The entry of profiles/<name> measured on this (n, q) and this build's device code
-    (nttmul.code_object_id), or None: a profile of another build is never reported."""
+def _profile_entry(name: str, n: int, q: int, kernels):
+    """The entry of profiles/<name> measured on this (n, q) with exactly these kernels:
+    `kernels` = {kernel_key: hash} of the kernels one step dispatches (nttmul.dispatched_kernel_
+    hashes), compared kernel by kernel with the entry's own "kernels" record.  A profile of any
+    other machine code -- or an entry without per-kernel hashes -- is never reported (fails
+    closed); edits of other kernels or of host code leave a matching entry valid."""
+    if not kernels:
+        return None
     try:
         data = json.load(open(os.path.join(ROOT, "profiles", name)))
     except (OSError, ValueError):
         return None
     for e in data.get("entries", []):
         if (e.get("n") == n and e.get("q") == q and e.get("batch")
-                and e.get("code_object") == code_object):
+                and e.get("kernels") == dict(kernels)):
             return e
     return None
 
 
-def load_traffic(n: int, q: int, batch: int, code_object: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary of this build
+def _kernels_tag(kernels) -> str:
+    return ", ".join(f"{k} {h}" for k, h in (kernels or {}).items()) or "none"
+
+
+def load_traffic(n: int, q: int, batch: int, kernels):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary of these kernels
     (profiles/pmc_traffic.json, tools/summarize_profile.py), scaled to this batch; with its
     source, or (None, reason)."""
-    e = _profile_entry("pmc_traffic.json", n, q, code_object)
+    e = _profile_entry("pmc_traffic.json", n, q, kernels)
     if e is None:
-        return None, f"no PMC profile of code object {code_object} at n={n}, q={q}"
+        return None, f"no PMC profile of kernels [{_kernels_tag(kernels)}] at n={n}, q={q}"
     return (e["hbm_bytes_per_launch"] * batch / e["batch"],
-            f"profiles/pmc_traffic.json <- {e['source']} (code object {code_object}, "
+            f"profiles/pmc_traffic.json <- {e['source']} (kernels {_kernels_tag(kernels)}; "
             f"batch {e['batch']}, {e['method']})")
 
 
-def load_valu_bound(n: int, q: int, code_object: str):
-    """VALU issue cycles per wave of the product kernel of this build, from its ISA listing
-    (profiles/valu_bound.json, tools/valu_bound.py), or None."""
-    return _profile_entry("valu_bound.json", n, q, code_object)
+def load_valu_bound(n: int, q: int, kernels):
+    """VALU issue cycles of one step's kernels, from their ISA listings (profiles/valu_bound.json,
+    tools/valu_bound.py), or None."""
+    return _profile_entry("valu_bound.json", n, q, kernels)
+
+
+def valu_roofline(vb: dict, count: int, kern_ms: float, source_kernels) -> dict:
+    """The bound that binds the product kernels: every dispatched kernel's ISA
+    listing priced at the measured issue costs (cycles per wave x waves per polynomial, summed
+    over the step's launches), for `count` polynomials over the 1,024 SIMDs at the 2.4 GHz
+    maximum clock; implied_clock_ghz = the clock at which the step would run exactly at it."""
+    per = []
+    total_cycles = 0.0
+    for k in vb["per_kernel"]:
+        w = k["waves_per_unit"] * count / SIMDS
+        total_cycles += k["cycles_per_wave"] * w
+        per.append({"kernel": k["kernel"], "valu_per_wave": k["valu_per_wave"],
+                    "cycles_per_wave": k["cycles_per_wave"], "waves_per_simd": w,
+                    "bound_ms": k["cycles_per_wave"] * w / (MAX_CLOCK_GHZ * 1e9) * 1e3})
+    bound_ms = total_cycles / (MAX_CLOCK_GHZ * 1e9) * 1e3
+    out = {"bound": "valu", "clock_ghz": MAX_CLOCK_GHZ, "bound_ms": bound_ms,
+           "frac": bound_ms / kern_ms, "cycles_per_simd": total_cycles,
+           "implied_clock_ghz": total_cycles / (kern_ms * 1e6), "kernels": per,
+           "source": f"profiles/valu_bound.json (kernels {_kernels_tag(source_kernels)}): each "
+                     "kernel's ISA listing priced at measured issue costs, summed over the step's "
+                     "launches, at the 2.4 GHz max clock; implied_clock_ghz = the clock at which "
+                     "the step would run exactly at that issue bound"}
+    if len(per) == 1:  # single-launch products: the per-wave figures at the top level as before
+        out.update(cycles_per_wave=per[0]["cycles_per_wave"],
+                   valu_per_wave=per[0]["valu_per_wave"], waves_per_simd=per[0]["waves_per_simd"])
+    return out
 
 
 def code_object_or_none():
@@ -339,6 +390,15 @@ def code_object_or_none():
     try:
         return nttmul.code_object_id()
     except (OSError, ValueError):
+        return None
+
+
+def kernels_or_none(names: str):
+    """{kernel_key: hash} of the kernels a step dispatches (nttmul_kernel_name string), or None."""
+    import nttmul
+    try:
+        return nttmul.dispatched_kernel_hashes(names)
+    except (OSError, ValueError, KeyError):
         return None
 
 
@@ -561,8 +621,9 @@ def main(argv=None):
 
     n, q = args.n, args.q
     wb = args.word_bits or (32 if q < (1 << 32) else 64)
-    # weak scaling: the same --batch-per-gpu at every N (C3's 65536 by default)
-    batch = args.batch_per_gpu
+    # per-GPU batch: --batch-per-gpu, else default_batch(world) -- C3's 65536 per
+    # GPU up to 4 ranks, C4's 2^20 / 8 at 8
+    batch = args.batch_per_gpu or default_batch(n, world)
     global_batch = batch * world
     p0, p1 = shard(global_batch, rank, world)
     count = p1 - p0
@@ -629,8 +690,8 @@ def main(argv=None):
         import numpy as np
         a, b, c = sets[(state["i"] - 1) % rotate]
         idx = sorted({0, 1, count // 2, count - 1})
-        host = c.view(count, n).cpu().numpy()
-        rows = host.view(np.uint32 if wb == 32 else np.uint64)[idx].astype(np.uint64)
+        host = c.view(count, n)[torch.tensor(idx, device=c.device)].cpu().numpy()
+        rows = host.view(np.uint32 if wb == 32 else np.uint64).astype(np.uint64)
         np.savez(f"{args.dump_samples}.rank{rank}.npz", p0=p0, p1=p1, idx=np.array(idx),
                  c=rows, n=n, q=q, world=world, global_batch=global_batch)
 
@@ -642,10 +703,13 @@ def main(argv=None):
         value = global_batch * args.steps / wall_max
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9     # GB/s
         product = args.op == "multiply"
-        single_launch = n <= 4096 and product
         co = code_object_or_none()
-        traffic, traffic_source = (load_traffic(n, q, count, co) if co and product else
-                                   (None, "no code object" if not co else "PMC profiles are of the product"))
+        kname = ((ctx.last_kernel_name() or ctx.kernel_name(wb, count)) if product
+                 else f"nttmul_{args.op}_batch_device")
+        kernels = kernels_or_none(kname) if product else None
+        traffic, traffic_source = (load_traffic(n, q, count, kernels) if kernels else
+                                   (None, "PMC profiles are of the product" if not product else
+                                    f"no per-kernel hashes for {kname}"))
         resident = alg_bytes * rotate <= IC_BYTES
         line = {
             "metric": METRIC if product else
@@ -672,18 +736,23 @@ def main(argv=None):
                                    f"(global {global_batch}), device-resident",
                        "op": args.op,
                        "n": n, "q": q, "batch_per_gpu": batch, "global_batch": global_batch,
-                       "parallelism": f"batch shards x{world}, no collective"},
+                       "parallelism": f"batch shards x{world}, no collective",
+                       "batch_rule": ("--batch-per-gpu" if args.batch_per_gpu else
+                                      "default: 65536 per GPU at 1/2/4 GPUs (C3 per GPU), "
+                                      "131072 at 8 (C4 = 2^20 across 8)")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": traffic_source,
-                         "kernel": ((ctx.last_kernel_name() or ctx.kernel_name(wb, count)) if product
-                                    else f"nttmul_{args.op}_batch_device"),
+                         "kernel": kname,
                          "kernel_ms": kern_ms,
                          "alg_bytes_per_launch": alg_bytes,
                          "buffer_sets": rotate,
                          "streams": nstreams,
                          "cache_resident": resident},
-            "build": {"code_object": co},
+            "build": {"code_object": co, "kernels": kernels,
+                      "note": "kernels: {kernel: sha256 of its machine code + descriptor} of the "
+                              "kernels one step dispatches (nttmul.kernel_hashes); the committed "
+                              "profiles below are looked up by these, kernel by kernel"},
             "cpu_baseline": None,
         }
         agg, per_rank = rank_summary(rank_rows, args.steps, words * n * wbytes, world, wall_max)
@@ -699,18 +768,9 @@ def main(argv=None):
                 f"one step's a, b, c ({alg_bytes / 2**20:.0f} MiB) fit the 256 MiB Infinity "
                 f"Cache; the steps cycle over {rotate} buffer sets ({rotate * alg_bytes / 2**20:.0f}"
                 " MiB) so inputs come from HBM as in a batch that does not fit")
-        vb = load_valu_bound(n, q, co) if (co and single_launch and wb == 32) else None
+        vb = load_valu_bound(n, q, kernels) if kernels else None
         if vb:  # the bound that binds: integer VALU issue, from this build's ISA
-            waves_per_simd = count * (n // 16) / 64 / SIMDS
-            bound_ms = vb["cycles_per_wave"] * waves_per_simd / (MAX_CLOCK_GHZ * 1e9) * 1e3
-            line["valu_roofline"] = {
-                "bound": "valu", "cycles_per_wave": vb["cycles_per_wave"],
-                "valu_per_wave": vb["valu_per_wave"], "waves_per_simd": waves_per_simd,
-                "clock_ghz": MAX_CLOCK_GHZ, "bound_ms": bound_ms, "frac": bound_ms / kern_ms,
-                "implied_clock_ghz": vb["cycles_per_wave"] * waves_per_simd / (kern_ms * 1e6),
-                "source": f"profiles/valu_bound.json (code object {co}): the ISA listing priced "
-                          "at measured issue costs, at the 2.4 GHz max clock; implied_clock_ghz "
-                          "= the clock at which the kernel would run exactly at that issue bound"}
+            line["valu_roofline"] = valu_roofline(vb, count, kern_ms, kernels)
         if world == 1 and args.power_seconds > 0:
             try:
                 props = torch.cuda.get_device_properties(dev)
@@ -737,8 +797,12 @@ def main(argv=None):
                 if vr and clk.get("clock_ghz_median"):  # the issue bound at the clock actually held
                     g = clk["clock_ghz_median"]
                     vr["in_kernel_clock_ghz"] = g
-                    vr["bound_ms_at_in_kernel_clock"] = vr["cycles_per_wave"] * vr["waves_per_simd"] / (g * 1e9) * 1e3
+                    vr["bound_ms_at_in_kernel_clock"] = vr["cycles_per_simd"] / (g * 1e9) * 1e3
                     vr["frac_at_in_kernel_clock"] = vr["bound_ms_at_in_kernel_clock"] / kern_ms
+                    if len(vr["kernels"]) > 1:
+                        vr["in_kernel_clock_note"] = (
+                            "the clock stamps are taken in the row pass (k_rows) only; the bound "
+                            "at that clock prices every launch of the step at it")
         if args.host_io and product:
             a, b, _ = sets[0]
             line["host_io"] = host_io(ctx, a, b, count, n, wb)

@@ -222,6 +222,179 @@ def code_object_id(path: str = LIB_PATH) -> str:
     return hashlib.sha256(fat if code is None else code).hexdigest()[:16]
 
 
+def _amdgcn_elfs(path: str) -> list:
+    """The gfx950 code objects (ELF images) of a HIP shared library's .hip_fatbin offload bundles."""
+    import struct
+    with open(path, "rb") as f:
+        elf = f.read()
+    fat = _elf_sections(elf).get(".hip_fatbin")
+    if fat is None:
+        raise ValueError(f"{path}: no .hip_fatbin section")
+    out, pos = [], fat.find(_BUNDLE_MAGIC)
+    while pos >= 0:
+        n, = struct.unpack_from("<Q", fat, pos + 24)
+        cur = pos + 32
+        for _ in range(n):
+            off, size, tlen = struct.unpack_from("<QQQ", fat, cur)
+            triple = fat[cur + 24:cur + 24 + tlen]
+            cur += 24 + tlen
+            if b"amdgcn" in triple and size:
+                out.append(fat[pos + off:pos + off + size])
+        pos = fat.find(_BUNDLE_MAGIC, cur)
+    return out
+
+
+def _elf_symbols(elf: bytes):
+    """(name, value, size, type, section index) of every .symtab entry of an ELF64 image, and the
+    (address, file offset) of each section."""
+    import struct
+    shoff, = struct.unpack_from("<Q", elf, 0x28)
+    shentsize, shnum, _ = struct.unpack_from("<HHH", elf, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQIIQQ", elf, shoff + i * shentsize) for i in range(shnum)]
+    syms = []
+    for s in secs:
+        if s[1] != 2:  # SHT_SYMTAB
+            continue
+        stroff = secs[s[6]][4]
+        for k in range(s[5] // 24):
+            name, info, _, shndx, value, size = struct.unpack_from("<IBBHQQ", elf, s[4] + 24 * k)
+            nm = elf[stroff + name:elf.index(b"\0", stroff + name)].decode(errors="replace")
+            syms.append((nm, value, size, info & 15, shndx))
+    return syms, [(s[3], s[4]) for s in secs]
+
+
+_BUILTIN = {"j": "u32", "m": "u64", "y": "u64", "i": "i32", "l": "i64", "b": "bool", "h": "u8"}
+
+
+def _demangle_args(s: str, i: int):
+    """Template arguments I...E of an Itanium-mangled nttmul kernel name from position i (at the
+    'I'), as short strings ("Arith32P3", "u32", "12", "false"); returns (args, next position) or
+    None for a form the kernels do not use."""
+    assert s[i] == "I"
+    i += 1
+    args = []
+    while s[i] != "E":
+        c = s[i]
+        if c in _BUILTIN:
+            args.append(_BUILTIN[c])
+            i += 1
+        elif c == "L":  # literal: L<type><value>E, n = negative
+            j = s.index("E", i)
+            t, v = s[i + 1], s[i + 2:j]
+            v = "-" + v[1:] if v.startswith("n") else v
+            args.append({"0": "false", "1": "true"}[v] if t == "b" else v)
+            i = j + 1
+        elif s.startswith("NS_", i):  # nttmul::<id>[<args>]
+            i += 3
+            j = i
+            while s[j].isdigit():
+                j += 1
+            ln = int(s[i:j])
+            name = s[j:j + ln]
+            i = j + ln
+            if s[i] == "I":
+                sub = _demangle_args(s, i)
+                if sub is None:
+                    return None
+                name += "<" + ",".join(sub[0]) + ">"
+                i = sub[1]
+            if s[i] != "E":
+                return None
+            i += 1
+            args.append(name)
+        else:
+            return None
+    return args, i + 1
+
+
+def kernel_key(symbol: str) -> str:
+    """Short name of a kernel symbol of libnttmul.so, e.g.
+    _ZN6nttmul6k_rowsINS_9Arith32P3EjjLi12ELi0ELb0EEEv... -> k_rows<Arith32P3,u32,u32,12,0,false>
+    (the mangled symbol itself for a form this small demangler does not cover)."""
+    if not symbol.startswith("_ZN6nttmul"):
+        return symbol
+    i = len("_ZN6nttmul")
+    j = i
+    while j < len(symbol) and symbol[j].isdigit():
+        j += 1
+    if j == i:
+        return symbol
+    ln = int(symbol[i:j])
+    name = symbol[j:j + ln]
+    k = j + ln
+    if k < len(symbol) and symbol[k] == "I":
+        try:
+            r = _demangle_args(symbol, k)
+        except (IndexError, KeyError, ValueError):
+            r = None
+        if r is None:
+            return symbol
+        return name + "<" + ",".join(r[0]) + ">"
+    return name
+
+
+def dispatch_key(name: str) -> str:
+    """The kernel_key of one kernel named the way the library's dispatch describes it
+    (nttmul_kernel_name: "k_rows<Arith32P3,u32,u32,12,0>", "...,prio>", "k_cols8<Arith64,u64,fwd>",
+    "k_cols_fwd<Arith64,u64,4>"): the template arguments the short names leave out are filled in
+    as kernels.hip instantiates them."""
+    import re
+    m = re.fullmatch(r"(\w+)<(.*)>", name.strip())
+    if not m:
+        return name.strip()
+    kern, args = m.group(1), m.group(2).split(",")
+    if kern == "k_rows":
+        prio = args[-1] == "prio"
+        args = (args[:-1] if prio else args) + ["true" if prio else "false"]
+    elif kern == "k_cols_fwd":
+        args = args + ["2"]
+    elif kern == "k_cols8":
+        w = "u64" if args[0] == "Arith64" else "u32"
+        args = ([args[0], args[1], w, "0", "2"] if args[2] == "fwd" else [args[0], w, args[1], "1", "1"])
+    return f"{kern}<{','.join(args)}>"
+
+
+def kernel_hashes(path: str = LIB_PATH) -> dict:
+    """Identity of every kernel in libnttmul.so's gfx950 code object, one by one: {kernel_key:
+    sha256 (16 hex digits) of the kernel's machine code (its .text range) and its 64-byte kernel
+    descriptor (<symbol>.kd: register, LDS, scratch and kernarg sizes), with the descriptor's
+    kernel_code_entry_byte_offset (bytes 16-23, the distance from descriptor to code, which moves
+    with every other kernel's size) zeroed}.  The kernels take everything through their arguments
+    (no PC-relative data: no s_getpc_b64 in the listing), so a kernel's bytes change only when
+    its own code does: a profile keyed by these hashes stays valid across edits of other kernels
+    and of host code, and a claim "kernel X unchanged" is checkable (code_object_id is the
+    whole-object digest)."""
+    import hashlib
+    out = {}
+    for co in _amdgcn_elfs(path):
+        syms, secs = _elf_symbols(co)
+        by_name = {s[0]: s for s in syms}
+        for nm, value, size, typ, shndx in syms:
+            if typ != 2 or not size or nm + ".kd" not in by_name:  # STT_FUNC with a descriptor
+                continue
+            addr, off = secs[shndx]
+            code = co[off + value - addr:off + value - addr + size]
+            kd = by_name[nm + ".kd"]
+            kaddr, koff = secs[kd[4]]
+            desc = bytearray(co[koff + kd[1] - kaddr:koff + kd[1] - kaddr + 64])
+            desc[16:24] = bytes(8)
+            out[kernel_key(nm)] = hashlib.sha256(code + bytes(desc)).hexdigest()[:16]
+    return out
+
+
+def dispatched_kernel_hashes(names: str, path: str = LIB_PATH) -> dict:
+    """{kernel_key: kernel hash}, in dispatch order, for a nttmul_kernel_name string
+    ("a + b + c"); raises KeyError naming a kernel the code object does not hold."""
+    table = kernel_hashes(path)
+    out = {}
+    for nm in (x.strip() for x in names.split("+")):
+        key = dispatch_key(nm)
+        if key not in table:
+            raise KeyError(f"{nm} ({key}) is not a kernel of {path}")
+        out[key] = table[key]
+    return out
+
+
 def exported_symbols() -> list:
     """Function names declared in include/nttmul.h (for the ABI completeness test)."""
     import re

@@ -98,17 +98,39 @@ def test_code_object_id(tmp_path):
 
 
 def test_profile_lookup_fails_closed(tmp_path, monkeypatch):
+    """Profiles are looked up kernel by kernel: an entry matches only when every kernel the step
+    dispatches has the hash the entry was measured on (no whole-code-object key)."""
     prof = tmp_path / "profiles"
     prof.mkdir()
-    entry = {"n": 4096, "q": 2013265921, "batch": 65536, "code_object": "aaaa",
+    ka = {"k_rows<A,u32,u32,12,0,false>": "aaaa"}
+    entry = {"n": 4096, "q": 2013265921, "batch": 65536, "kernels": ka,
              "hbm_bytes_per_launch": 2.0e9, "source": "x_pmc.json", "method": "m"}
-    (prof / "pmc_traffic.json").write_text(json.dumps({"entries": [entry]}))
+    legacy = dict(entry, kernels=None, code_object="aaaa", hbm_bytes_per_launch=9.0)
+    (prof / "pmc_traffic.json").write_text(json.dumps({"entries": [legacy, entry]}))
     monkeypatch.setattr(bench, "ROOT", str(tmp_path))
-    t, src = bench.load_traffic(4096, 2013265921, 32768, "aaaa")
+    t, src = bench.load_traffic(4096, 2013265921, 32768, ka)
     assert t == 1.0e9 and "aaaa" in src                            # scaled to the batch
-    t, src = bench.load_traffic(4096, 2013265921, 65536, "bbbb")   # another build
-    assert t is None and "bbbb" in src
-    assert bench.load_valu_bound(4096, 2013265921, "aaaa") is None  # no file: None
+    t, src = bench.load_traffic(4096, 2013265921, 65536, {"k_rows<A,u32,u32,12,0,false>": "bbbb"})
+    assert t is None and "bbbb" in src                             # that kernel changed
+    two = dict(ka, **{"k_cols8<A,u64,u64,1,1>": "cccc"})
+    assert bench.load_traffic(4096, 2013265921, 65536, two)[0] is None   # a kernel more
+    assert bench.load_traffic(4096, 2013265921, 65536, None)[0] is None
+    assert bench.load_valu_bound(4096, 2013265921, ka) is None      # no file: None
+
+
+def test_valu_roofline_sums_the_launches():
+    """valu_roofline: cycles per wave x waves per polynomial, summed over a step's launches."""
+    vb = {"per_kernel": [{"kernel": "a", "valu_per_wave": 10, "cycles_per_wave": 100.0,
+                          "waves_per_unit": 64},
+                         {"kernel": "b", "valu_per_wave": 20, "cycles_per_wave": 300.0,
+                          "waves_per_unit": 64}]}
+    vr = bench.valu_roofline(vb, 1024, 1.0, {"a": "1", "b": "2"})
+    cyc = (100.0 + 300.0) * 64 * 1024 / bench.SIMDS
+    assert vr["cycles_per_simd"] == pytest.approx(cyc)
+    assert vr["bound_ms"] == pytest.approx(cyc / 2.4e9 * 1e3) and vr["frac"] == vr["bound_ms"]
+    assert [k["kernel"] for k in vr["kernels"]] == ["a", "b"] and "cycles_per_wave" not in vr
+    one = bench.valu_roofline({"per_kernel": vb["per_kernel"][:1]}, 65536, 2.0, {"a": "1"})
+    assert one["cycles_per_wave"] == 100.0 and one["waves_per_simd"] == 64 * 65536 / 1024
 
 
 def test_power_probe_summary():
@@ -154,10 +176,17 @@ def test_c1_single_product_line():
     assert c1["us_per_polymult"] == pytest.approx(1e6 / c1["value"])
 
 
-def test_weak_scaling_batch_is_constant():
-    """--batch-per-gpu is the same at every N (no switch to C4's slice at 8 ranks)."""
-    assert bench.parse([]).batch_per_gpu == 65536
-    assert bench.parse(["--gpus", "8"]).batch_per_gpu == 65536
+def test_default_batch_per_gpu():
+    """--batch-per-gpu defaults to C3's 65536 per GPU at 1, 2 and 4 ranks and to C4's
+    2^20 / 8 at 8 ranks, so the driver's 8-GPU line is BASELINE configs[3] (verdict r5 item 4)."""
+    assert bench.parse([]).batch_per_gpu is None
+    assert bench.parse(["--batch-per-gpu", "7"]).batch_per_gpu == 7
+    for world, per in ((1, 65536), (2, 65536), (4, 65536), (8, 131072)):
+        assert bench.default_batch(4096, world) == per
+    assert bench.workload_name(4096, 2013265921, 8 * bench.default_batch(4096, 8), 8) == "C4"
+    assert bench.workload_name(4096, 2013265921, bench.default_batch(4096, 1), 1) == "C3"
+    assert bench.workload_name(4096, 2013265921, 4 * bench.default_batch(4096, 4), 4) == "C3"
+    assert bench.default_batch(65536, 8) == 65536     # other n: the explicit flag sets the load
 
 
 def test_settle_runs_untimed_chunks_until_the_wall_time():
@@ -190,16 +219,106 @@ def test_op_defaults_to_the_product():
         bench.parse(["--op", "square"])
 
 
-def test_committed_profiles_describe_the_shipped_library():
-    """The driver's bench line reads traffic and valu_roofline from the committed profiles only
-    when they were measured on this build's code object (bench.py fails closed otherwise): the
-    in-tree libnttmul.so must have a PMC entry for C3, C2 and C5 and a VALU bound for C3 / C2."""
+# what the library dispatches for the three bench configurations (pinned on the GPU by
+# tests/test_gpu_parity.py::test_dispatch_names_of_the_bench_configs)
+BENCH_DISPATCH = {
+    (4096, 2013265921, 65536): "k_rows<Arith32P3,u32,u32,12,0>",
+    (1024, 2013265921, 4096): "k_rows<Arith32P,u32,u32,10,0,prio>",
+    (65536, 0x3FFFFFFFFFE80001, 1024):
+        "k_cols8<Arith64,u64,fwd> + k_rows<Arith64,u64,u64,8,8> + k_cols8<Arith64,u64,inv>",
+}
+
+
+def test_committed_profiles_describe_the_shipped_kernels():
+    """Each committed profile entry bench.py reports for C3, C2 and C5 (PMC traffic and the VALU
+    bound) was measured on exactly the kernels the in-tree libnttmul.so dispatches: every entry's
+    per-kernel hash equals the in-tree kernel's (nttmul.kernel_hashes).  A device-code edit of a
+    product kernel fails this until that configuration is re-profiled; edits of other kernels or
+    of host code do not (verdict r5 item 1)."""
     if not os.path.exists(nttmul.LIB_PATH):
         pytest.skip("libnttmul.so not built")
-    co = nttmul.code_object_id()
-    for n, q, batch in ((4096, 2013265921, 65536), (1024, 2013265921, 4096),
-                        (65536, 0x3FFFFFFFFFE80001, 1024)):
-        traffic, why = bench.load_traffic(n, q, batch, co)
+    for (n, q, batch), names in BENCH_DISPATCH.items():
+        kernels = nttmul.dispatched_kernel_hashes(names)
+        traffic, why = bench.load_traffic(n, q, batch, kernels)
         assert traffic is not None, why
-    for n in (4096, 1024):
-        assert bench.load_valu_bound(n, 2013265921, co) is not None, f"no VALU bound of {co} at n={n}"
+        vb = bench.load_valu_bound(n, q, kernels)
+        assert vb is not None, f"no VALU bound of {kernels} at n={n}"
+        assert [k["kernel"] for k in vb["per_kernel"]] == list(kernels)
+
+
+def _code_object(funcs) -> bytes:
+    """A minimal amdgcn-like ELF64: .text holding each (name, code) back to back, .rodata one
+    64-byte descriptor <name>.kd per kernel (entry offset = distance to its code), .symtab."""
+    text, rodata, syms = b"", b"", []
+    strtab = b"\0"
+    for name, code in funcs:
+        syms.append((len(strtab), 0x12, 2, len(text), len(code)))           # FUNC in .text
+        strtab += name.encode() + b"\0"
+        kd = bytearray(64)
+        struct.pack_into("<q", kd, 16, len(text) - len(rodata))             # moves with layout
+        kd[48:52] = b"rsrc"
+        syms.append((len(strtab), 0x11, 3, len(rodata), 64))                # OBJECT in .rodata
+        strtab += (name + ".kd").encode() + b"\0"
+        text += code
+        rodata += bytes(kd)
+    symtab = bytes(24) + b"".join(struct.pack("<IBBHQQ", nm, info, 0, sec, val, size)
+                                  for nm, info, sec, val, size in syms)
+    secs = [(".text", 1, text, 0), (".rodata", 1, rodata, 0), (".strtab", 3, strtab, 0),
+            (".symtab", 2, symtab, 4)]  # section 0 null, 1 .shstrtab, 2.. these
+    names = b"\0.shstrtab\0" + b"".join(k.encode() + b"\0" for k, _, _, _ in secs)
+    off = 64 + len(names)
+    body = bytearray(64) + names
+    heads = [struct.pack("<IIQQQQIIQQ", 0, 0, 0, 0, 0, 0, 0, 0, 0, 0),
+             struct.pack("<IIQQQQIIQQ", 1, 3, 0, 0, 64, len(names), 0, 0, 1, 0)]
+    name_off = 11
+    for k, typ, data, link in secs:
+        heads.append(struct.pack("<IIQQQQIIQQ", name_off, typ, 0, 0, off, len(data), link, 0, 8,
+                                 24 if typ == 2 else 0))
+        name_off += len(k) + 1
+        body += data
+        off += len(data)
+    sh_off = off + (-off) % 8
+    body += bytes(sh_off - len(body))
+    body[:4] = b"\x7fELF"
+    body[4], body[5] = 2, 1
+    struct.pack_into("<Q", body, 0x28, sh_off)
+    struct.pack_into("<HHH", body, 0x3A, 64, len(heads), 1)
+    return bytes(body) + b"".join(heads)
+
+
+def test_kernel_hashes_are_per_kernel(tmp_path):
+    """nttmul.kernel_hashes: one hash per kernel over its own code and descriptor; growing another
+    kernel (which moves every later kernel and its descriptor's entry offset) changes only that
+    kernel's hash; the short names follow the template arguments."""
+    rows = "_ZN6nttmul6k_rowsINS_9Arith32P3EjjLi12ELi0ELb0EEEvNS_7KParamsIT_EEPKT0_S7_PT1_m"
+    cols = "_ZN6nttmul7k_cols8INS_7Arith64EmmLi1ELi1EEEvNS_7KParamsIT_EEPKT0_S7_PS5_S8_m"
+
+    def lib(path, first):
+        _elf_with_fatbin(path, _bundle([(b"hipv4-amdgcn-amd-amdhsa--gfx950",
+                                         _code_object([(cols, first), (rows, b"\x11" * 32)]))]))
+        return nttmul.kernel_hashes(str(path))
+    a = lib(tmp_path / "a.so", b"\x22" * 16)
+    b = lib(tmp_path / "b.so", b"\x22" * 48)                          # k_cols8 grew
+    assert set(a) == {"k_rows<Arith32P3,u32,u32,12,0,false>", "k_cols8<Arith64,u64,u64,1,1>"}
+    assert a["k_rows<Arith32P3,u32,u32,12,0,false>"] == b["k_rows<Arith32P3,u32,u32,12,0,false>"]
+    assert a["k_cols8<Arith64,u64,u64,1,1>"] != b["k_cols8<Arith64,u64,u64,1,1>"]
+
+
+def test_dispatch_names_map_to_kernels():
+    """nttmul.dispatch_key fills in the template arguments the dispatch's short names omit, and
+    every bench configuration's kernels exist in the built library."""
+    assert nttmul.dispatch_key("k_rows<Arith32P,u32,u32,10,0,prio>") == \
+        "k_rows<Arith32P,u32,u32,10,0,true>"
+    assert nttmul.dispatch_key("k_rows<Arith32P3,u32,u32,12,0>") == \
+        "k_rows<Arith32P3,u32,u32,12,0,false>"
+    assert nttmul.dispatch_key("k_cols8<Arith64,u64,fwd>") == "k_cols8<Arith64,u64,u64,0,2>"
+    assert nttmul.dispatch_key("k_cols8<Arith64,u32,inv>") == "k_cols8<Arith64,u64,u32,1,1>"
+    assert nttmul.dispatch_key("k_cols_fwd<Arith32P,u32,4>") == "k_cols_fwd<Arith32P,u32,4,2>"
+    assert nttmul.kernel_key("_ZN6nttmul10k_cols_fwdINS_8Arith32TILb1EEEmLi2ELi2EEEvNS_7KParams"
+                             "IT_EEPKT0_S8_PNS4_4wordESA_mi") == "k_cols_fwd<Arith32T<true>,u64,2,2>"
+    if not os.path.exists(nttmul.LIB_PATH):
+        pytest.skip("libnttmul.so not built")
+    table = nttmul.kernel_hashes()
+    assert not [k for k in table if k.startswith("_Z")]              # every kernel demangled
+    for names in BENCH_DISPATCH.values():
+        assert len(nttmul.dispatched_kernel_hashes(names)) == len(names.split("+"))

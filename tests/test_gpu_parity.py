@@ -49,6 +49,17 @@ def test_native_library_is_loaded_and_on_gpu(torch_cuda):
     assert os.path.samefile(nttmul.LIB_PATH, nttmul.load_library()._name)
 
 
+def test_dispatch_names_of_the_bench_configs(torch_cuda):
+    """The kernels the library dispatches for the bench's C3, C2 and C5 batches are the ones the
+    CPU suite's BENCH_DISPATCH table names (tests/test_bench_host.py), whose per-kernel hashes key
+    the committed profiles; each is a kernel of the loaded library."""
+    from test_bench_host import BENCH_DISPATCH
+    for (n, q, batch), names in BENCH_DISPATCH.items():
+        ctx = _ctx(n, q)
+        assert ctx.kernel_name(batch=batch) == names, (n, q, batch)
+        assert len(nttmul.dispatched_kernel_hashes(names)) == len(names.split("+"))
+
+
 def _kats(golden_dir):
     data = json.load(open(os.path.join(golden_dir, "kat256.json")))
     for kat in data["kats"]:
@@ -778,7 +789,15 @@ def test_small_server_yields_to_other_work(torch_cuda):
     anything else, and the kernel leaves 1 ms after its last request, so (1) a device-API product
     of the same context, (2) a torch kernel and synchronize on the default stream and (3) another
     context's server call from another thread, each issued right after a server call, finish far
-    below the old 20 ms idle window -- and every result stays exact."""
+    below the old 20 ms idle window -- and every result stays exact.
+    (2) has a control (verdict r5 item 5): the same torch kernel and synchronize with no server
+    resident (the context's device-API call stops it first), interleaved with the timed ones; the
+    after-server median may exceed the control median by less than 2 ms.  Round 5's one failure
+    here (93.10 ms for (2), the device-API call of the same run 0.10 ms) was torch's first launch
+    of its own add / sum kernels in the process -- code-object load and allocator warm-up, a
+    one-time cost that the timed loop met in its first iteration -- which is why torch's kernels
+    run once before anything is timed."""
+    import statistics
     import threading
     import time
     torch = torch_cuda
@@ -795,7 +814,15 @@ def test_small_server_yields_to_other_work(torch_cuda):
     (da + 1).sum()                      # torch's own kernels loaded before anything is timed
     ctx.multiply_device(dc, da, db, 1, 32, stream=s)
     torch.cuda.synchronize()
-    worst = {}
+    worst, after, control = {}, [], []
+
+    def torch_op():
+        t0 = time.perf_counter()
+        x = (da + 1).sum()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        assert int(x) == int(da.sum()) + n
+        return dt
     for it in range(10):
         ctx.multiply(a, b)
         assert ctx.last_host_path() == 3
@@ -804,12 +831,11 @@ def test_small_server_yields_to_other_work(torch_cuda):
         torch.cuda.synchronize()
         worst["device_api"] = max(worst.get("device_api", 0), time.perf_counter() - t0)
         assert np.array_equal(dc.cpu().numpy().view(np.uint32).astype(np.uint64), exp)
+        control.append(torch_op())                          # control: no server resident
         ctx.multiply(a, b)
-        t0 = time.perf_counter()
-        x = (da + 1).sum()                                  # (2) foreign work + device sync
-        torch.cuda.synchronize()
-        worst["torch_sync"] = max(worst.get("torch_sync", 0), time.perf_counter() - t0)
-        assert int(x) == int(da.sum()) + n
+        assert ctx.last_host_path() == 3
+        after.append(torch_op())                            # (2) right after a server call
+    worst["torch_sync"] = max(after)
     other = _ctx(512, q)
     a2, b2 = O.fill_inputs(512, q, 7, 1)
     P2 = O.Plan(512, q)
@@ -828,7 +854,12 @@ def test_small_server_yields_to_other_work(torch_cuda):
         worst["other_context"] = max(worst.get("other_context", 0), res["t"])
         assert np.array_equal(res["c"][0].astype(np.uint64), P2.product_merged(a2[0], b2[0]))
         assert other.last_host_path() == 3
-    assert all(t < 5e-3 for t in worst.values()), {k: f"{v * 1e3:.2f} ms" for k, v in worst.items()}
+    report = {k: f"{v * 1e3:.2f} ms" for k, v in worst.items()}
+    report["torch after server / control, medians"] = (
+        f"{statistics.median(after) * 1e3:.3f} / {statistics.median(control) * 1e3:.3f} ms")
+    assert statistics.median(after) - statistics.median(control) < 2e-3, report
+    # worst cases: below the old 20 ms idle window with room for host scheduling jitter (advisor r5)
+    assert all(t < 15e-3 for t in worst.values()), report
 
 
 @pytest.mark.parametrize("n,q,batch", [(4096, Q31, 1537), (256, Q30, 20000), (1024, Q62, 1100),
@@ -942,7 +973,7 @@ def test_transform_modes_device(torch_cuda):
         assert torch.equal(back, a)
 
 
-@pytest.mark.parametrize("world,batch", [(2, 4096), (8, 1024)])
+@pytest.mark.parametrize("world,batch", [(2, 4096), (8, 1024), (8, None)])
 def test_bench_ranks_on_one_gpu(world, batch, tmp_path, torch_cuda):
     """bench.py's N > 1 path as the driver launches it (torch.distributed.run, one process per
     rank, gloo control plane: barrier + all_reduce(MAX) + all_gather), with every rank on this
@@ -951,7 +982,8 @@ def test_bench_ranks_on_one_gpu(world, batch, tmp_path, torch_cuda):
     roofline (all ranks' bytes over the max-over-ranks wall time against N x 8 TB/s) and rank 0's
     CPU baseline with its cores (run after the final barrier at every N, verdict r4 item 2); the
     products each rank dumps from its own contiguous slice [k batch, (k + 1) batch)
-    equal the oracle's at their global counter positions."""
+    equal the oracle's at their global counter positions.  batch None: the driver's default
+    arguments at 8 ranks, which run C4 (2^20 across 8, 131,072 per rank; verdict r5 item 4)."""
     import socket
     import subprocess
     import sys
@@ -964,11 +996,18 @@ def test_bench_ranks_on_one_gpu(world, batch, tmp_path, torch_cuda):
         [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
          str(world), "--master-addr", "127.0.0.1", "--master-port", str(port),
          os.path.join(root, "bench.py"), "--gpus", str(world), "--steps", "3", "--warmup", "1",
-         "--settle-ms", "20", "--cpu-seconds", "0.5", "--batch-per-gpu", str(batch),
-         "--dump-samples", prefix],
+         "--settle-ms", "20", "--cpu-seconds", "0.5", "--dump-samples", prefix]
+        + (["--batch-per-gpu", str(batch)] if batch else []),
         capture_output=True, text=True, timeout=300, cwd=root)
     assert out.returncode == 0, out.stderr[-3000:]
     line = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    if batch is None:  # default arguments: C4 at 8 ranks
+        batch = 131072
+        assert line["config"]["workload"].startswith("C4: ")
+        assert line["config"]["global_batch"] == 1 << 20
+        assert line["config"]["batch_rule"].startswith("default")
+    else:
+        assert line["config"]["batch_rule"] == "--batch-per-gpu"
     assert line["n_gpus"] == world and line["config"]["global_batch"] == world * batch
     assert line["config"]["batch_per_gpu"] == batch and line["value"] > 0
     assert line["scaling"] == "weak"

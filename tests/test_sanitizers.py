@@ -36,16 +36,18 @@ def test_asan_ubsan_host_code(tmp_path):
 
 @pytest.mark.skipif(shutil.which("g++") is None, reason="no g++")
 def test_tsan_copy_pool(tmp_path):
-    """csrc/copy_pool.hpp (the host-buffer path's split staging copies, rewritten in round 5 with
-    lazily started workers and one condition variable per worker) under ThreadSanitizer: four
-    caller threads share the process-wide pool with varied sizes and split counts; every copy is
-    compared byte for byte (tests/sanitize/tsan_copy_pool.cpp)."""
+    """csrc/copy_pool.hpp (the host-buffer path's split staging copies; round 6: concurrent calls
+    share the workers through a job queue instead of queueing on one call lock) under
+    ThreadSanitizer: four caller threads start together and share the process-wide pool with
+    varied sizes (3 MiB + 2 among them: the ceiling split) and split counts; every copy is
+    compared byte for byte, and the run fails unless at least two split copies were in flight at
+    once (tests/sanitize/tsan_copy_pool.cpp)."""
     exe = tmp_path / "tsan_copy_pool"
     subprocess.run(["g++", "-std=c++17", "-fsanitize=thread", "-g", "-O1", "-I", CSRC, "-o",
                     str(exe), os.path.join(ROOT, "tests", "sanitize", "tsan_copy_pool.cpp"),
                     "-pthread"], check=True)
     env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1")
-    env.pop("LD_PRELOAD", None)
-    out = subprocess.run([str(exe), "4", "40"], capture_output=True, text=True, timeout=300, env=env)
+    out = subprocess.run([str(exe), "4", "40", "2"], capture_output=True, text=True, timeout=300,
+                         env=env)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
     assert "copy pool tsan run ok" in out.stdout

@@ -50,6 +50,11 @@ json.dump(out, open(dst + "_pmc.json", "w"), indent=1)
 
 cfg = bench["config"]
 entry_co = bench.get("build", {}).get("code_object")
+# the kernels one step dispatches, {kernel_key: hash of its machine code} (bench.py build.kernels):
+# bench.py looks the entry up by these, kernel by kernel
+entry_kernels = bench.get("build", {}).get("kernels")
+if not entry_kernels:
+    sys.exit("bench line without build.kernels (per-kernel hashes): profile a current bench.py")
 main = "k_rows" if "k_rows" in out else sorted(out)[0]
 m = out[main]
 # one step = one dispatch of each product kernel (k_rows; plus k_cols_fwd/k_cols_inv for n > 4096)
@@ -60,9 +65,9 @@ tpath = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 table = json.load(open(tpath)) if os.path.exists(tpath) else {"entries": []}
 table["entries"] = [e for e in table["entries"]
                     if not (e["n"] == cfg["n"] and e["q"] == cfg["q"] and e["batch"] == cfg["batch_per_gpu"]
-                            and e.get("code_object") == entry_co)]
+                            and e.get("kernels") == entry_kernels)]
 entry = {"n": cfg["n"], "q": cfg["q"], "batch": cfg["batch_per_gpu"], "kernel": "+".join(step_kernels),
-         "code_object": bench.get("build", {}).get("code_object"),
+         "code_object": entry_co, "kernels": entry_kernels,
          "hbm_bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
          "alg_bytes_per_launch": bench["roofline"]["alg_bytes_per_launch"],
          "traffic_over_alg": (fetch + write) / bench["roofline"]["alg_bytes_per_launch"],
