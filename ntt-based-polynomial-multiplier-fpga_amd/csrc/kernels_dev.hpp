@@ -616,6 +616,55 @@ __device__ __forceinline__ void inv_all(const KParams<A> &P, typename A::word (&
 // performed stage is a residue mod x^(2^D) - w (x^(2^D) + w): z = +-w, the twiddle already in
 // zw.  The last group always starts at a multiple of 16 elements, so bit D of a register's
 // offset says X or Y.  Same canonical output as the full transform (the product is unique).
+// base_mult with the blocks by compile-time recursion over the register index K0 instead of an
+// unrolled loop, for Arith32P3 (NTTMUL_P3_PIN): its base multiplication pins the halfway fold
+// with an empty asm, and a loop holding inline asm is not fully unrolled (its register indices
+// turn into runtime ones).  The other classes keep the loop (the recursion reorders their code:
+// +15 VALU in the C5 row pass)
+template <class A, int LOGS, int D, int K0 = 0>
+__device__ __forceinline__ void base_mult_rec(const A &ar, typename A::word (&x)[16],
+                                          const typename A::word (&y)[16],
+                                          const TwPair<typename A::word> (&zw)[16], int j) {
+  using Gr = Groups<LOGS, kWT<A, LOGS>()>;
+  constexpr int g = Gr::G - 1, B = 1 << D;
+  static_assert(D == 0 || Gr::S(g) > D, "last register group too short for the base blocks");
+  if constexpr (D == 0) {
+#pragma unroll
+    for (int k = 0; k < 16; k++) x[k] = ar.mont(x[k], y[k]);
+  } else if constexpr (K0 < 16) {
+    constexpr int o0 = Gr::off(g, K0);
+    if constexpr ((o0 & (B - 1)) == 0) {  // K0 holds a block's constant coefficient
+      int r[B];
+#pragma unroll
+      for (int i = 0; i < B; i++) r[i] = Gr::reg_of(g, o0 + i);
+      constexpr bool neg = (o0 >> D) & 1;
+      constexpr int kz = Gr::reg_of(g, o0 & ~B);
+      TwPair<typename A::word> z = zw[kz];
+      // typed arithmetic: the last forward stage (dist 8 >> (S - D - 1)) multiplied N-type
+      // operands, and so kept the centred twiddle, when bit 2 dist of its X register is set
+      constexpr int dl = 8 >> (Gr::S(g) - D - 1);
+      // (Arith32P, NTTMUL_P_TYPED 2: the same condition says the pair is in signed form)
+      constexpr bool typed_z = A::kTyped || (kTypedP<A>() && NTTMUL_P_TYPED >= 2);
+      // (kWT, when that stage was its group's first: the pair is in signed form exactly when the
+      // wave's elements were the previous group's differences.  The signed-input product is
+      // exact for canonical inputs too, so every wave takes it: the unsigned pair of the other
+      // waves becomes the signed one by b1 + (b0 >> 31), two instructions, instead of a second
+      // copy of the base multiplication behind a branch)
+      constexpr bool kWtFirst = kWT<A, LOGS>() && Gr::S(g) - D - 1 == 0;
+      if constexpr (kWtFirst)
+        z.ws += (typename A::word)((z.w >> 31) & (1 - Gr::wave_type(j)));
+      constexpr bool zc = typed_z && (kWtFirst || (Gr::S(g) - D - 1 > 0 && (kz & (2 * dl))));
+      typename A::word a[B], b[B];
+#pragma unroll
+      for (int i = 0; i < B; i++) a[i] = x[r[i]], b[i] = y[r[i]];
+      ar.template basemul<B, neg, zc>(a, b, z.w, z.ws);
+#pragma unroll
+      for (int i = 0; i < B; i++) x[r[i]] = a[i];
+    }
+    base_mult_rec<A, LOGS, D, K0 + 1>(ar, x, y, zw, j);
+  }
+}
+
 template <class A, int LOGS, int D>
 __device__ __forceinline__ void base_mult(const A &ar, typename A::word (&x)[16],
                                           const typename A::word (&y)[16],
@@ -626,6 +675,8 @@ __device__ __forceinline__ void base_mult(const A &ar, typename A::word (&x)[16]
   if constexpr (D == 0) {
 #pragma unroll
     for (int k = 0; k < 16; k++) x[k] = ar.mont(x[k], y[k]);
+  } else if constexpr (std::is_same<A, Arith32P3>::value && NTTMUL_P3_PIN) {
+    base_mult_rec<A, LOGS, D>(ar, x, y, zw, j);
   } else {
 #pragma unroll
     for (int k0 = 0; k0 < 16; k0++) {
@@ -806,7 +857,7 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
 #pragma unroll
       for (int k = 0; k < 16; k++) {
         W v = x[k];
-        if (!A::kInvCanonical) v = P.ar.canon(v);
+        if (!A::kInvCanonical) v = P.ar.canon_inv(v);
         buf_st32<kAuxSt>(rc, (Gr::base(0, j) + Gr::off(0, k)) * 4, (uint32_t)v);
       }
     }
@@ -818,7 +869,7 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
 #pragma unroll
     for (int k = 0; k < 16; k++) {
       W v = x[k];
-      if (L1 == 0 && !A::kInvCanonical) v = P.ar.canon(v);
+      if (L1 == 0 && !A::kInvCanonical) v = P.ar.canon_inv(v);
       st_stream<kNT>(c + base_w + Gr::off(0, k) * kRS, (TOut)v);
     }
   }
@@ -1149,7 +1200,7 @@ __global__ __launch_bounds__(LOGS == 8 ? 512 : LOGS == 9 ? 64 : 128) void k_serv
 #pragma unroll
           for (int k = 0; k < 16; k++) {
             W v = x[k];
-            if (!A::kInvCanonical) v = P.ar.canon(v);
+            if (!A::kInvCanonical) v = P.ar.canon_inv(v);
             sc[Gr::base(0, j) + Gr::off(0, k)] = v;
           }
           xsync<1>();
@@ -1212,7 +1263,7 @@ __global__ __launch_bounds__(LOGS == 8 ? 512 : LOGS == 9 ? 64 : 128) void k_serv
 #pragma unroll
         for (int k = 0; k < 16; k++) {
           W v = x[k];
-          if (!A::kInvCanonical) v = P.ar.canon(v);
+          if (!A::kInvCanonical) v = P.ar.canon_inv(v);
           sc[base + Gr::off(0, k)] = v;
         }
       }
@@ -1299,7 +1350,10 @@ __global__ __launch_bounds__(256) void k_xform(KParams<A> P, const TIn *__restri
 #pragma unroll
     for (int k = 0; k < 16; k++) {
       W v = x[k];
-      if (DIR == 0 || (L1 == 0 && !A::kInvCanonical)) v = P.ar.canon(v);
+      if (DIR == 0)
+        v = P.ar.canon(v);
+      else if (L1 == 0 && !A::kInvCanonical)
+        v = P.ar.canon_inv(v);
       out[base_out + Gr::off(GOUT, k) * kRSO] = (TOut)v;
     }
   }
@@ -1308,7 +1362,10 @@ __global__ __launch_bounds__(256) void k_xform(KParams<A> P, const TIn *__restri
 #pragma unroll
     for (int k = 0; k < 16; k++) {
       W v = y[k];
-      if (DIR == 0 || !A::kInvCanonical) v = P.ar.canon(v);
+      if (DIR == 0)
+        v = P.ar.canon(v);
+      else if (!A::kInvCanonical)
+        v = P.ar.canon_inv(v);
       out[base_out + Gr::off(GOUT, k)] = (TOut)v;
     }
   }
@@ -1324,7 +1381,7 @@ __global__ __launch_bounds__(256) void k_pointwise(KParams<A> P, const IO *__res
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
   const W t = P.ar.mont((W)a[i], (W)b[i]);
-  c[i] = (IO)P.ar.canon(P.ar.mont(t, P.f));
+  c[i] = (IO)P.ar.canon_inv(P.ar.mont(t, P.f));  // mont: [0, 2q)
 }
 
 // Column pass, forward: global stages 0..L1-1 of CT on a and b.  Thread = one column
@@ -1401,7 +1458,7 @@ __global__ __launch_bounds__(256) void k_cols_inv(KParams<A> P,
 #pragma clang loop unroll(full)
   for (int m = 0; m < M; m++)
     st_stream<NTTMUL_NT_COLS>(c + base + ((size_t)m << logs),
-                              (TOut)(A::kInvCanonical ? x[m] : P.ar.canon(x[m])));
+                              (TOut)(A::kInvCanonical ? x[m] : P.ar.canon_inv(x[m])));
 }
 
 // Column pass of the square split n = 2^8 x 2^8 (n = 65536, NTTMUL_C5_SQ): each column of 256
@@ -1463,7 +1520,7 @@ __global__ __launch_bounds__(256) void k_cols8(KParams<A> P, const TIn *__restri
     for (int k = 0; k < 16; k++) {
       const size_t o = (size_t)(Gr::base(GOUT, jj) + Gr::off(GOUT, k)) << 8;
       st_stream<NTTMUL_NT_COLS>(ta + base + o,
-                                (TOut)(A::kInvCanonical ? x[k] : P.ar.canon(x[k])));
+                                (TOut)(A::kInvCanonical ? x[k] : P.ar.canon_inv(x[k])));
     }
   }
 }

@@ -227,6 +227,8 @@ struct Arith32T {
   __device__ __forceinline__ uint32_t canon(uint32_t x) const {
     return H ? csub(csub(x, 2 * q), q) : csub(x, q);
   }
+  // an inverse transform's output -> [0, q) (see Arith64::canon_inv; unchanged here)
+  __device__ __forceinline__ uint32_t canon_inv(uint32_t x) const { return canon(x); }
 
   // Base multiplication of the incomplete transform (kernels.hip base_mult): a = a b 2^-32 in
   // Z_q[x]/(x^B - z), z = (NEG ? -1 : 1) w for the Montgomery-form twiddle (w1, w2).  Inputs
@@ -312,6 +314,9 @@ using Arith32H = Arith32T<true>;   // q < 2^30
 #endif
 #ifndef NTTMUL_P_FOLD  // Arith32P base multiplication: fold the sum's high word by 2^32 mod q
 #define NTTMUL_P_FOLD 1
+#endif
+#ifndef NTTMUL_P3_PIN  // Arith32P3 base multiplication: pin the halfway fold (empty asm)
+#define NTTMUL_P3_PIN 1
 #endif
 struct Arith32P {
   using word = uint32_t;
@@ -413,6 +418,7 @@ struct Arith32P {
   }
   // [0, 2q) -> [0, q)
   __device__ __forceinline__ uint32_t canon(uint32_t x) const { return csub(x, q); }
+  __device__ __forceinline__ uint32_t canon_inv(uint32_t x) const { return csub(x, q); }
 
   // Base multiplication (see Arith32T::basemul): a = a b 2^-32 in Z_q[x]/(x^4 - z), z = +-w.
   // a, b in [0, 2q) from the forward transform; z b_i by Plantard (canonical straight from any
@@ -515,19 +521,31 @@ struct Arith32P3 : Arith32P {
       const uint32_t t = ZC ? pmul_s(br[i], w0, w1) : pmul(kN ? br[i] : b[i], w0, w1);
       bz[i] = NEG ? q - t : t;
     }
-#pragma unroll
-    for (int k = 0; k < B; k++) {
+    outputs<B, 0>(a, ar, br, bz);
+  }
+  // output K of the 8 x 8 block (compile-time recursion over K, see kernels_dev.hpp base_mult)
+  template <int B, int K>
+  __device__ __forceinline__ void outputs(uint32_t (&a)[B], const uint32_t (&ar)[B],
+                                          const uint32_t (&br)[B], const uint32_t (&bz)[B]) const {
+    if constexpr (K < B) {
       uint64_t s = 0;
 #pragma unroll
       for (int i = 0; i < B / 2; i++)
-        s += (uint64_t)ar[i] * (i <= k ? br[k - i] : bz[B + k - i]);
+        s += (uint64_t)ar[i] * (i <= K ? br[K - i] : bz[B + K - i]);
       s = (uint64_t)(uint32_t)(s >> 32) * c32 + (uint32_t)s;
+#if NTTMUL_P3_PIN
+      // the folded first half is the addend of the second half's multiply-add chain; without
+      // the pin LLVM re-associates the second half into a fresh chain and adds the fold after
+      // it (a v_mov + v_lshl_add_u64 more per output)
+      asm("" : "+v"(s));
+#endif
 #pragma unroll
       for (int i = B / 2; i < B; i++)
-        s += (uint64_t)ar[i] * (i <= k ? br[k - i] : bz[B + k - i]);
+        s += (uint64_t)ar[i] * (i <= K ? br[K - i] : bz[B + K - i]);
       const uint64_t s2 = (uint64_t)(uint32_t)(s >> 32) * c32 + (uint32_t)s;
       const uint32_t m = (uint32_t)s2 * qinv_neg;
-      a[k] = csub((uint32_t)((s2 + (uint64_t)m * q) >> 32), q);
+      a[K] = csub((uint32_t)((s2 + (uint64_t)m * q) >> 32), q);
+      outputs<B, K + 1>(a, ar, br, bz);
     }
   }
 };
@@ -591,6 +609,7 @@ struct Arith32W {
     return redc(p, (uint32_t)p * qinv_neg);
   }
   __device__ __forceinline__ uint32_t canon(uint32_t x) const { return x; }
+  __device__ __forceinline__ uint32_t canon_inv(uint32_t x) const { return x; }
   static constexpr int kBaseD = 0;  // sums of two canonical products already exceed 2^64
   template <int B, bool NEG, bool ZC = false>
   __device__ void basemul(uint32_t (&)[B], const uint32_t (&)[B], uint32_t, uint32_t) const {}
@@ -617,6 +636,11 @@ struct Arith32W {
 // high product through the carry-out of v_mad_u64_u32 (Arith64::mulhi64; tools/kbench A/B)
 #ifndef NTTMUL_A64_MADC
 #define NTTMUL_A64_MADC 1
+#endif
+// inverse outputs canonicalised by one conditional subtraction (Arith64::canon_inv; tools/kbench
+// A/B: 0 restores canon's two)
+#ifndef NTTMUL_A64_CANON_INV
+#define NTTMUL_A64_CANON_INV 1
 #endif
 // CT sum output through the Shoup product's addend (Arith64::ct; tools/kbench A/B)
 #ifndef NTTMUL_A64_ACC
@@ -745,6 +769,7 @@ struct Arith64 {
     Y = shoup(x - y + q, wf, wfs);
   }
   __device__ __forceinline__ uint64_t canon(uint64_t x) const { return csub(x, q); }
+  __device__ __forceinline__ uint64_t canon_inv(uint64_t x) const { return csub(x, q); }
 #else
   static constexpr uint64_t kLazy = 4;  // forward values in [0, 4q), inverse values in [0, 2q)
   // Harvey CT: X in [0, 4q), any Y -> outputs in [0, 4q).  NTTMUL_A64_ACC: the sum comes out of
@@ -777,6 +802,13 @@ struct Arith64 {
   }
   // [0, 4q) -> [0, q)
   __device__ __forceinline__ uint64_t canon(uint64_t x) const { return csub(csub(x, 2 * q), q); }
+  // [0, 2q) -> [0, q): every value an inverse transform outputs, and every Montgomery product, is
+  // below 2q (GS: csub(x + y, 2q) and Shoup products of x, y < 2q; base multiplication and mont:
+  // (S + m q) / 2^64 < 2q), so one conditional subtraction canonicalises it where canon's two
+  // (for the forward transform's [0, 4q)) were spent before round 6
+  __device__ __forceinline__ uint64_t canon_inv(uint64_t x) const {
+    return NTTMUL_A64_CANON_INV ? csub(x, q) : canon(x);
+  }
 #endif
   // Montgomery a b 2^-64 mod q; a, b lazy (< kLazy q) -> [0, 2q).  q < 2^62.
   __device__ __forceinline__ uint64_t mont(uint64_t a, uint64_t b) const {

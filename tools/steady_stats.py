@@ -4,7 +4,7 @@ including the first ≈ 40 ms of the card's clock ramp, come before them).  rocp
 --stats average covers every dispatch, ramp included; this gives the steady-state figure the
 bench line's event-timed kernel_ms measures, from the same trace.
 
-    python tools/r5/steady_stats.py <kernel_trace.csv> <K> [out.json]
+    python tools/steady_stats.py <kernel_trace.csv> <K> [out.json]
 
 Same-named kernels launched in a fixed order per step (the multi-pass product's two k_cols8
 passes) are told apart by their Kernel_Id order, as tools/summarize_profile.py does."""
