@@ -1,8 +1,8 @@
 """C3 energy budget (verdict r4 item 3): does static power x time + memory energy + the kernel
 listing priced at measured per-instruction energies add up to the bench line's board energy per
-product?  Inputs are one GPU session's files (tools/r5/gpu_r5b.sh) plus the C3 kernel's listing
+product?  Inputs are one GPU session's files (round 5: tools/r5/gpu_r5b.sh, archived, tools/archive/MANIFEST.md) plus the C3 kernel's listing
 (hipcc -S of csrc/kernels.hip, the library's code object):
-    python tools/r5/energy_summary.py gpurun_out/r5b build/kernels.s profiles/r5/c3_energy_budget.json
+    python tools/energy/c3_energy_summary.py gpurun_out/r5b build/kernels.s profiles/r5/c3_energy_budget.json
 Every energy is 'above sleep': board power minus the power with every wave resident and sleeping,
 per unit of work; the sleeping board (clock tree, leakage, fabric and HBM standby at that clock)
 is charged as static power over the product's time.  The per-instruction energies come from
@@ -191,7 +191,7 @@ out = {
         "sum / measured": total / board_uj},
     "ablations_kbench": abl,
     "operating_point_fit": fit,
-    "source": f"{src}: energy.json (tools/r5/energy_budget.py), c3_bench.json (bench.py), "
+    "source": f"{src}: energy.json (tools/energy/energy_microbench.py), c3_bench.json (bench.py), "
               "c3abl/ (kbench + amd-smi); listing: hipcc -S of csrc/kernels.hip",
 }
 os.makedirs(os.path.dirname(dst), exist_ok=True)

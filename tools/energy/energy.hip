@@ -1,5 +1,5 @@
 // Board energy of the work classes in the C3 product kernel (verdict r4 item 3: the C3 energy
-// budget).  tools/r5/energy_budget.py runs each kind back to back for a few seconds while it
+// budget).  tools/energy/energy_microbench.py runs each kind back to back for a few seconds while it
 // samples board power in process (amdsmi) and divides power by the kind's rate.
 //   VALU kinds: CH independent chains per lane, 8 waves per SIMD, operands kept random by xor
 //   feedback (round 4's chained v_mul_hi collapsed to zero, profiles/r4/energy/); a kind's

@@ -1,12 +1,13 @@
 """Board energy of each work class in the C3 product kernel (verdict r4 item 3), measured on the
-GPU box: every kind of tools/r5/energy.hip runs back to back for --seconds while bench.power_probe
+GPU box: every kind of tools/energy/energy.hip runs back to back for --seconds while bench.power_probe
 samples socket power in process (amdsmi), the rate comes from wall time over the same launches
 and the clock from the kernel's own s_memtime / s_memrealtime stamps.  Reports per kind the board
 power, the clock, and energies above the all-waves-sleeping board power:
   VALU: pJ per lane-op of the instruction itself (the pair kinds minus their xor refresh),
   LDS:  pJ per lane-op of ds_write_b32 / ds_read_b32 (their xor removed),
   memory: pJ per byte read / written / copied from HBM, per byte read from L2.
-    python tools/r5/energy_budget.py [--seconds 3] > energy.json"""
+    python tools/energy/energy_microbench.py [--seconds 3] > energy.json   (build libenergy.so first:
+    hipcc --offload-arch=gfx950 -O3 -shared -fPIC tools/energy/energy.hip -o tools/energy/libenergy.so)"""
 import argparse
 import ctypes
 import json
@@ -51,7 +52,7 @@ kinds = [int(k) for k in args.kinds.split(",")] if args.kinds else list(range(li
 ITERS = {"sleep": 4096, "hbm_read_16B_nt": 128, "hbm_write_16B_nt": 128, "hbm_copy_16B_nt": 64,
          "l2_read_16B": 4096, "ds_write_b32+ds_read_b32+xor": 2048}
 res = {"blocks": blocks, "threads": 256, "device": props.name,
-       "source": "tools/r5/energy.hip kinds, board power by amdsmi in process (bench.power_probe)",
+       "source": "tools/energy/energy.hip kinds, board power by amdsmi in process (bench.power_probe)",
        "kinds": {}}
 for k in kinds:
     name = names[k]

@@ -2,7 +2,7 @@
 ntt256_product4 shape) through the resident device server vs a kernel launch per call, and the
 server's own timeline from lib/libnttmul_diag.so (nttmul_diag_server_stamps): request seen ->
 a, b loaded -> product computed -> c stored and released, plus the host's go -> done-seen time.
-    python tools/r4/server_latency.py [--calls 2000] > out.json"""
+    python tools/server_latency.py [--calls 2000] > out.json"""
 import argparse
 import ctypes
 import json
@@ -11,7 +11,7 @@ import statistics
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "ntt-based-polynomial-multiplier-fpga_amd"))
 import numpy as np  # noqa: E402
 import nttmul  # noqa: E402

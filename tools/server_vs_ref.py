@@ -3,7 +3,7 @@ reference's own timing loop (time_testing256.c:175-187, as apps/time_testing_gpu
 relinked against libnttmul's ntt256_product4, 2,000 calls) against the reference's compiled
 ntt256_product4 on one core of the same host (oracle/ref_anchor.c over oracle/_ref), three runs
 each, interleaved, in one JSON:
-    python tools/r5/server_vs_ref.py > profiles/r5/server_vs_ref_<box>.json
+    python tools/server_vs_ref.py > profiles/r5/server_vs_ref_<box>.json
 No GPU work in this process: the harness runs as a child program."""
 import json
 import os
@@ -12,7 +12,7 @@ import socket
 import subprocess
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from oracle import oracle as O  # noqa: E402
 
