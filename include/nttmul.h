@@ -99,7 +99,12 @@ typedef struct {
 
 /* ≙ PCIE_Load + PCIE_Open + mode-0 parameter/twiddle stream (NTT_PCIECommunicationv2.c:137-178) */
 int nttmul_create(nttmul_ctx **ctx, uint32_t n, uint64_t q, int ndev);
-/* the fields n .. flags of *params (NTTMUL_PARAMS_BASE_SIZE bytes); the knobs take defaults */
+/* the fields n .. flags of *params (NTTMUL_PARAMS_BASE_SIZE bytes); the knobs take defaults.
+ * Compatibility note (advisor r5): in round 4 this entry point also read the knob fields
+ * (issue_prio .. small_server).  Since round 5 it reads the round 1-3 layout only, so a binary
+ * built against the round-4 header that sets those knobs through nttmul_create_ex gets their
+ * defaults without an error: such a binary must be rebuilt to call nttmul_create_sized with
+ * sizeof(nttmul_params). */
 int nttmul_create_ex(nttmul_ctx **ctx, const nttmul_params *params);
 /* the first params_size bytes of *params, the rest defaults: pass sizeof(nttmul_params) to set
  * the knobs.  NTTMUL_EINVAL for params_size below NTTMUL_PARAMS_BASE_SIZE or above the size this
@@ -130,6 +135,12 @@ int nttmul_last_kernel_name(const nttmul_ctx *ctx, char *buf, size_t cap);
  * the pinned staging buffers, 3 the resident device server's mailbox (params.small_server);
  * -1 before any call. */
 int nttmul_last_host_path(const nttmul_ctx *ctx);
+/* Diagnostics: setup or launch failures of the context's device server (params.small_server) so
+ * far (>= 0; NTTMUL_EINVAL without a context), and the last one's message in reason (cap bytes,
+ * "" when none): the call that met the failure ran on the launch path instead, an out-of-memory
+ * failure retries the server after 64 more eligible calls (up to 3 failures), any other failure
+ * leaves the launch path for the context's lifetime. */
+int nttmul_server_status(const nttmul_ctx *ctx, char *reason, size_t cap);
 
 /* multiply(a, b, n, q) -> c for one polynomial; host buffers of n words.
  * ≙ mode-1 + mode-2 + mode-3 + FIFO read of NTT_HARDWARE_EXE (NTT_PCIECommunicationv2.c:183-224) */

@@ -92,6 +92,10 @@ struct Server {
   uint64_t host_ns = 0;                       // go -> done seen on the host, last request
   bool running = false;                       // launched and not known to have left
   std::chrono::steady_clock::time_point launched, last_done;
+  // setup / launch failures (server_unavailable): how many, the last one's message, and how many
+  // more eligible calls take the launch path before the server is tried again (advisor r5)
+  unsigned failures = 0, cooldown = 0;
+  char reason[192] = {0};
 };
 // The resident kernel occupies its hardware queue (4 per process on the box) while it waits, so
 // work other streams place in that queue -- and a device-wide synchronize -- waits behind it.  It
@@ -556,13 +560,34 @@ int server_alloc(nttmul_ctx *ctx, DevState &d) {
 // idle exit.
 int server_quiesce(nttmul_ctx *ctx) { return ctx->server.running ? server_stop(ctx) : NTTMUL_OK; }
 
-// The server cannot run for this context (setup or launch refused, e.g. no fine-grained memory
-// or an unsupported table): every later small call takes the launch path.
-int server_unavailable(nttmul_ctx *ctx) {
-  ctx->small_server = -1;
-  ctx->server.running = false;
+// The server could not be set up or launched (status st: the runtime refused an allocation,
+// a launch, ...): this call takes the launch path.  The failure is kept for nttmul_server_status
+// (count and message) instead of vanishing with the cleared error string: an out-of-memory
+// failure retries the server after the next 64 eligible calls, up to 3 failures in all; any other
+// failure, or the third, leaves the launch path for the context's lifetime.
+constexpr unsigned kServerRetryCalls = 64, kServerMaxFailures = 3;
+int server_unavailable(nttmul_ctx *ctx, int st) {
+  Server &S = ctx->server;
+  S.running = false;
   (void)hipGetLastError();
-  set_err(ctx, "");  // (the failure that led here is handled: the launch path runs)
+  S.failures++;
+  const bool retry = st == NTTMUL_ENOMEM && S.failures < kServerMaxFailures;
+  {
+    std::lock_guard<std::mutex> l(g_err_mu);
+    char msg[sizeof(ctx->err)];
+    snprintf(msg, sizeof(msg), "%s", ctx->err);
+    if (retry)
+      snprintf(S.reason, sizeof(S.reason), "failure %u (%s): %s; retried after %u calls", S.failures,
+               nttmul_strerror(st), msg, kServerRetryCalls);
+    else
+      snprintf(S.reason, sizeof(S.reason), "failure %u (%s): %s; launch path from now on",
+               S.failures, nttmul_strerror(st), msg);
+    ctx->err[0] = 0;  // (the call itself succeeds on the launch path)
+  }
+  if (retry)
+    S.cooldown = kServerRetryCalls;
+  else
+    ctx->small_server = -1;
   return 1;
 }
 
@@ -583,14 +608,24 @@ int run_server(nttmul_ctx *ctx, void *c, const void *a, const void *b, size_t ba
       }
   }
   Server &S = ctx->server;
+  if (S.cooldown) {  // after a transient setup failure (server_unavailable)
+    S.cooldown--;
+    return 1;
+  }
   DevState &d = ctx->dev[0];
-  if (!S.req && server_alloc(ctx, d)) return server_unavailable(ctx);
+  if (!S.req) {
+    const int st = server_alloc(ctx, d);
+    if (st) return server_unavailable(ctx, st);
+  }
   const auto now = std::chrono::steady_clock::now();
   if (S.running && (now - S.last_done > kServerIdleHost || now - S.launched > kServerLifeHost)) {
     const int st = server_stop(ctx);
     if (st) return st;
   }
-  if (!S.running && server_launch(ctx, d)) return server_unavailable(ctx);
+  if (!S.running) {
+    const int st = server_launch(ctx, d);
+    if (st) return server_unavailable(ctx, st);
+  }
   // Completion is the result itself: c is set to a word no product can hold (the server's
   // q < 2^31, so 0xFFFFFFFF) before go, and the request is done when no word of c still holds it.
   // Every 4-byte store of the kernel lands whole, so this needs no release fence and no done word
@@ -620,8 +655,9 @@ int run_server(nttmul_ctx *ctx, void *c, const void *a, const void *b, size_t ba
       // this request after the check above, or it left before it saw it -- then relaunch
       if (landed()) break;
       S.running = false;
-      // (a relaunch the runtime refuses: this request and every later one take the launch path)
-      if (server_launch(ctx, d)) return server_unavailable(ctx);
+      // (a relaunch the runtime refuses: this request takes the launch path)
+      const int st = server_launch(ctx, d);
+      if (st) return server_unavailable(ctx, st);
     } else if (q != hipErrorNotReady) {
       S.running = false;
       return fail(ctx, q, "device server");
@@ -874,6 +910,12 @@ int nttmul_get_info(const nttmul_ctx *ctx, nttmul_info *info) {
 }
 
 int nttmul_last_host_path(const nttmul_ctx *ctx) { return ctx ? ctx->last_path : NTTMUL_EINVAL; }
+
+int nttmul_server_status(const nttmul_ctx *ctx, char *reason, size_t cap) {
+  if (!ctx) return NTTMUL_EINVAL;
+  if (reason && cap) snprintf(reason, cap, "%s", ctx->server.reason);
+  return (int)ctx->server.failures;
+}
 
 int nttmul_kernel_name_batch(const nttmul_ctx *ctx, int word_bits, size_t batch, char *buf,
                              size_t cap) {

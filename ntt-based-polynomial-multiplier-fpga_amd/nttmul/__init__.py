@@ -119,6 +119,7 @@ def _bind(lib: ctypes.CDLL) -> ctypes.CDLL:
     lib.nttmul_kernel_name_batch.argtypes = [vp, i32, sz, ctypes.c_char_p, sz]
     lib.nttmul_last_kernel_name.argtypes = [vp, ctypes.c_char_p, sz]
     lib.nttmul_last_host_path.argtypes = [vp]
+    lib.nttmul_server_status.argtypes = [vp, ctypes.c_char_p, sz]
     for name in ("nttmul_multiply_u32", "nttmul_multiply_u64"):
         getattr(lib, name).argtypes = [vp, vp, vp, vp]
     for name in ("nttmul_multiply_batch_u32", "nttmul_multiply_batch_u64"):
@@ -493,6 +494,15 @@ class Context:
         """nttmul_last_host_path: 0 staged, 1 direct DMA, 2 zero-copy, 3 device server, -1 no
         call yet."""
         return int(self._lib.nttmul_last_host_path(self._h))
+
+    def server_status(self):
+        """nttmul_server_status: (setup / launch failures of the device server so far, the last
+        one's message)."""
+        buf = ctypes.create_string_buffer(256)
+        n = self._lib.nttmul_server_status(self._h, buf, len(buf))
+        if n < 0:
+            self._check(n)
+        return int(n), buf.value.decode()
 
     def kernel_name(self, word_bits: int = 0, batch: int = 0) -> str:
         """The device kernel(s) a product call of `batch` polynomials dispatches to

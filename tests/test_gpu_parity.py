@@ -854,6 +854,7 @@ def test_small_server_yields_to_other_work(torch_cuda):
         worst["other_context"] = max(worst.get("other_context", 0), res["t"])
         assert np.array_equal(res["c"][0].astype(np.uint64), P2.product_merged(a2[0], b2[0]))
         assert other.last_host_path() == 3
+    assert ctx.server_status() == (0, "") and other.server_status() == (0, "")   # no fallback
     report = {k: f"{v * 1e3:.2f} ms" for k, v in worst.items()}
     report["torch after server / control, medians"] = (
         f"{statistics.median(after) * 1e3:.3f} / {statistics.median(control) * 1e3:.3f} ms")
