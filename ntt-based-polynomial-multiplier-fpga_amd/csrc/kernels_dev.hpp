@@ -323,14 +323,20 @@ template <class T>
 __device__ __forceinline__ auto span_rsrc(const T *p, size_t words) {
   return __builtin_amdgcn_make_buffer_rsrc((void *)p, 0, (int)(words * sizeof(T)), 0x00020000);
 }
+// SOFF: a wave-uniform byte offset passed as the instruction's scalar offset (NTTMUL_BUF_SOFF:
+// the register's constant part, so the per-lane offset is the thread's base alone and no VALU
+// add / or forms each register's address)
 template <int AUX, class R>
-__device__ __forceinline__ uint32_t buf_ld32(R r, int byte_off) {
-  return __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, AUX);
+__device__ __forceinline__ uint32_t buf_ld32(R r, int byte_off, int soff = 0) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, soff, AUX);
 }
 template <int AUX, class R>
-__device__ __forceinline__ void buf_st32(R r, int byte_off, uint32_t v) {
-  __builtin_amdgcn_raw_buffer_store_b32(v, r, byte_off, 0, AUX);
+__device__ __forceinline__ void buf_st32(R r, int byte_off, uint32_t v, int soff = 0) {
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, byte_off, soff, AUX);
 }
+#ifndef NTTMUL_BUF_SOFF
+#define NTTMUL_BUF_SOFF 1
+#endif
 
 // One forward CT stage l of group g on NPOLY (1 or 2) polynomials (same twiddles); the twiddles
 // of the group's last performed stage are kept in zw[X register] (see base_mult).  TIN: under the
@@ -730,6 +736,15 @@ __device__ __forceinline__ void base_mult(const A &ar, typename A::word (&x)[16]
 __host__ __device__ constexpr int rows_threads(int logs) {
   return NTTMUL_SMALL_BLOCK && logs == 10 ? 64 : 256;
 }
+// __launch_bounds__ minimum waves per SIMD of k_rows: NTTMUL_MIN_WAVES, and for the one-wave
+// n = 1024 products NTTMUL_MIN_WAVES_1024 (8: 64 VGPRs instead of 84-86, so a launch's four waves
+// per SIMD at C2 leave room for the next launch's four on another stream)
+#ifndef NTTMUL_MIN_WAVES_1024
+#define NTTMUL_MIN_WAVES_1024 NTTMUL_MIN_WAVES
+#endif
+__host__ __device__ constexpr int rows_min_waves(int logs) {
+  return NTTMUL_SMALL_BLOCK && logs == 10 ? NTTMUL_MIN_WAVES_1024 : NTTMUL_MIN_WAVES;
+}
 // Square split (k_cols8): the intermediates ta, tb, tc tiled per 16 columns (NTTMUL_C5_TILE), so
 // the column passes store / load one contiguous 32 KiB tile per workgroup and the row pass moves
 // 512 contiguous bytes per instruction, instead of 128-byte runs 2 KiB apart (a row-major
@@ -775,7 +790,7 @@ __device__ __forceinline__ void clk_stamp(int k) {
 #endif
 
 template <class A, class TIn, class TOut, int LOGS, int L1, bool PRIO = false>
-__global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
+__global__ __launch_bounds__(rows_threads(LOGS), rows_min_waves(LOGS)) void k_rows(
     KParams<A> P, const TIn *__restrict__ a, const TIn *__restrict__ b, TOut *__restrict__ c,
     size_t units) {
   using W = typename A::word;
@@ -824,9 +839,15 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
     } else {
 #pragma unroll
       for (int k = 0; k < 16; k++) {
-        const int off = (Gr::base(0, j) + Gr::off(0, k)) * 4;
-        x[k] = (W)buf_ld32<kAux>(ra, off);
-        y[k] = (W)buf_ld32<kAux>(rb, off);
+        if constexpr (NTTMUL_BUF_SOFF) {
+          const int vo = Gr::base(0, j) * 4, so = Gr::off(0, k) * 4;
+          x[k] = (W)buf_ld32<kAux>(ra, vo, so);
+          y[k] = (W)buf_ld32<kAux>(rb, vo, so);
+        } else {
+          const int off = (Gr::base(0, j) + Gr::off(0, k)) * 4;
+          x[k] = (W)buf_ld32<kAux>(ra, off);
+          y[k] = (W)buf_ld32<kAux>(rb, off);
+        }
       }
     }
   } else {
@@ -858,7 +879,10 @@ __global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(
       for (int k = 0; k < 16; k++) {
         W v = x[k];
         if (!A::kInvCanonical) v = P.ar.canon_inv(v);
-        buf_st32<kAuxSt>(rc, (Gr::base(0, j) + Gr::off(0, k)) * 4, (uint32_t)v);
+        if constexpr (NTTMUL_BUF_SOFF)
+          buf_st32<kAuxSt>(rc, Gr::base(0, j) * 4, (uint32_t)v, Gr::off(0, k) * 4);
+        else
+          buf_st32<kAuxSt>(rc, (Gr::base(0, j) + Gr::off(0, k)) * 4, (uint32_t)v);
       }
     }
     CLK_STAMP(1);

@@ -9,14 +9,14 @@ import sys
 R = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 s = open(os.path.join(R, "ntt-based-polynomial-multiplier-fpga_amd", "csrc", "kernels_dev.hpp")).read()
 head = ("template <class A, class TIn, class TOut, int LOGS, int L1, bool PRIO = false>\n"
-        "__global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows(\n"
+        "__global__ __launch_bounds__(rows_threads(LOGS), rows_min_waves(LOGS)) void k_rows(\n"
         "    KParams<A> P, const TIn *__restrict__ a, const TIn *__restrict__ b, TOut *__restrict__ c,\n"
         "    size_t units) {")
 a = s.index(head)
 b = s.index("  CLK_STAMP(1);\n}\n", a) + len("  CLK_STAMP(1);\n}\n")
 body = s[a + len(head):b]
 out = ("template <class A, class TIn, class TOut, int LOGS, int L1, bool PRIO = false>\n"
-       "__global__ __launch_bounds__(rows_threads(LOGS), NTTMUL_MIN_WAVES) void k_rows_pl(\n"
+       "__global__ __launch_bounds__(rows_threads(LOGS), rows_min_waves(LOGS)) void k_rows_pl(\n"
        "    const TIn *__restrict__ a, const TIn *__restrict__ b, TOut *__restrict__ c,\n"
        "    size_t units, KParams<A> P) {" + body)
 dst = sys.argv[1] if len(sys.argv) > 1 else os.path.join(R, "tools", "kbench", "bin")
