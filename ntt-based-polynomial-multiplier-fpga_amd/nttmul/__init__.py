@@ -119,7 +119,8 @@ def _bind(lib: ctypes.CDLL) -> ctypes.CDLL:
     lib.nttmul_kernel_name_batch.argtypes = [vp, i32, sz, ctypes.c_char_p, sz]
     lib.nttmul_last_kernel_name.argtypes = [vp, ctypes.c_char_p, sz]
     lib.nttmul_last_host_path.argtypes = [vp]
-    lib.nttmul_server_status.argtypes = [vp, ctypes.c_char_p, sz]
+    if hasattr(lib, "nttmul_server_status"):  # (round 6; tools/bench_ab.py loads older builds)
+        lib.nttmul_server_status.argtypes = [vp, ctypes.c_char_p, sz]
     for name in ("nttmul_multiply_u32", "nttmul_multiply_u64"):
         getattr(lib, name).argtypes = [vp, vp, vp, vp]
     for name in ("nttmul_multiply_batch_u32", "nttmul_multiply_batch_u64"):
