@@ -30,10 +30,7 @@ for cfg in $CFGS; do
     c3) one c3 ;;
     c5) one c5 --n 65536 --q 4611686018425815041 --batch-per-gpu 1024 --steps 200 --warmup 100 ;;
     c2) one c2 --n 1024 --batch-per-gpu 4096 --steps 3000 --warmup 2000 ;;
-    c2s) mkdir -p gpurun_out/$TAG/c2s  # two streams: bench line only (same kernel as c2)
-         run 300 python bench.py --n 1024 --batch-per-gpu 4096 --steps 3000 --warmup 2000 --streams 2 \
-           --no-cpu-baseline > gpurun_out/$TAG/c2s/bench.json 2> gpurun_out/$TAG/c2s/bench.err
-         tail -c 400 gpurun_out/$TAG/c2s/bench.json >&2 ;;
+    c2s) one c2s --n 1024 --batch-per-gpu 4096 --steps 3000 --warmup 2000 --streams 2 ;;  # two streams: the oldest-first kernel
   esac
 done
 echo "done $TAG" >&2
