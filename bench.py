@@ -709,9 +709,12 @@ def main(argv=None):
         kname = ((ctx.last_kernel_name() or ctx.kernel_name(wb, count)) if product
                  else f"nttmul_{args.op}_batch_device")
         kernels = kernels_or_none(kname) if product else None
-        traffic, traffic_source = (load_traffic(n, q, count, kernels) if kernels else
+        traffic, traffic_source = (load_traffic(n, q, count, kernels) if kernels and nstreams == 1 else
                                    (None, "PMC profiles are of the product" if not product else
-                                    f"no per-kernel hashes for {kname}"))
+                                    "not attributable: with launches overlapping on several "
+                                    "streams each dispatch's counter window holds the others' "
+                                    "traffic too (2.01 x at C2, profiles/r6/c2s_pmc.json)"
+                                    if nstreams > 1 else f"no per-kernel hashes for {kname}"))
         resident = alg_bytes * rotate <= IC_BYTES
         line = {
             "metric": METRIC if product else
