@@ -622,22 +622,20 @@ __device__ __forceinline__ void inv_all(const KParams<A> &P, typename A::word (&
 // performed stage is a residue mod x^(2^D) - w (x^(2^D) + w): z = +-w, the twiddle already in
 // zw.  The last group always starts at a multiple of 16 elements, so bit D of a register's
 // offset says X or Y.  Same canonical output as the full transform (the product is unique).
-// base_mult with the blocks by compile-time recursion over the register index K0 instead of an
-// unrolled loop, for Arith32P3 (NTTMUL_P3_PIN): its base multiplication pins the halfway fold
-// with an empty asm, and a loop holding inline asm is not fully unrolled (its register indices
-// turn into runtime ones).  The other classes keep the loop (the recursion reorders their code:
-// +15 VALU in the C5 row pass)
+//
+// base_mult_rec: the same with the blocks by compile-time recursion over the register index K0
+// instead of an unrolled loop, for Arith32P3 (NTTMUL_P3_PIN; base_mult below dispatches to it):
+// its base multiplication pins the halfway fold with an empty asm, and a loop holding inline asm
+// is not fully unrolled (its register indices turn into runtime ones).  The other classes keep
+// the loop (for them the recursion only reorders the code: +15 VALU in the C5 row pass).
 template <class A, int LOGS, int D, int K0 = 0>
 __device__ __forceinline__ void base_mult_rec(const A &ar, typename A::word (&x)[16],
                                           const typename A::word (&y)[16],
                                           const TwPair<typename A::word> (&zw)[16], int j) {
   using Gr = Groups<LOGS, kWT<A, LOGS>()>;
   constexpr int g = Gr::G - 1, B = 1 << D;
-  static_assert(D == 0 || Gr::S(g) > D, "last register group too short for the base blocks");
-  if constexpr (D == 0) {
-#pragma unroll
-    for (int k = 0; k < 16; k++) x[k] = ar.mont(x[k], y[k]);
-  } else if constexpr (K0 < 16) {
+  static_assert(D > 0 && Gr::S(g) > D, "base blocks of 2^D > 1 coefficients in the last group");
+  if constexpr (K0 < 16) {
     constexpr int o0 = Gr::off(g, K0);
     if constexpr ((o0 & (B - 1)) == 0) {  // K0 holds a block's constant coefficient
       int r[B];
@@ -737,8 +735,9 @@ __host__ __device__ constexpr int rows_threads(int logs) {
   return NTTMUL_SMALL_BLOCK && logs == 10 ? 64 : 256;
 }
 // __launch_bounds__ minimum waves per SIMD of k_rows: NTTMUL_MIN_WAVES, and for the one-wave
-// n = 1024 products NTTMUL_MIN_WAVES_1024 (8: 64 VGPRs instead of 84-86, so a launch's four waves
-// per SIMD at C2 leave room for the next launch's four on another stream)
+// n = 1024 products NTTMUL_MIN_WAVES_1024 (an A/B switch: 8 gives 64 VGPRs instead of 84-86, so
+// the next C2 launch's four waves per SIMD fit beside the running four on another stream, but
+// measured +3.2 % on one stream and +3.6 % on two; default: no bound)
 #ifndef NTTMUL_MIN_WAVES_1024
 #define NTTMUL_MIN_WAVES_1024 NTTMUL_MIN_WAVES
 #endif

@@ -908,6 +908,27 @@ def test_host_path_pinned_direct(n, q, batch, torch_cuda):
     assert np.array_equal(c2.astype(np.uint64), ref) and ctx.last_host_path() == 1
 
 
+def test_bench_host_io_leg(torch_cuda):
+    """bench.py --host-io's leg (the PCIe-inclusive rate, never the bench value): the pageable
+    call writes into the caller's reused output array, the page-locked call runs the direct-DMA
+    branch, and both give the device path's products."""
+    import bench
+    torch = torch_cuda
+    n, q, batch = 4096, Q31, 1000                       # 15.6 MiB per operand: two chunks
+    ctx = _ctx(n, q)
+    a = torch.empty(batch * n, dtype=torch.int32, device="cuda")
+    b, c = torch.empty_like(a), torch.empty_like(a)
+    s = torch.cuda.current_stream().cuda_stream
+    ctx.fill_random_device(a, b, 5, batch, 32, stream=s)
+    ctx.multiply_device(c, a, b, batch, 32, stream=s)
+    torch.cuda.synchronize()
+    line = bench.host_io(ctx, a, b, batch, n, 32, reps=2)
+    assert line["value"] > 0 and line["pinned"].get("matches_pageable") is True, line
+    got = ctx.multiply(a.cpu().numpy().view(np.uint32).reshape(batch, n),
+                       b.cpu().numpy().view(np.uint32).reshape(batch, n))
+    assert np.array_equal(got, c.cpu().numpy().view(np.uint32).reshape(batch, n))
+
+
 # ---------------------------------------------------------------------------------------------
 # The reference's whole transform wrapper set (NTT/ntt256.h:20-69) and its general form
 # ---------------------------------------------------------------------------------------------
