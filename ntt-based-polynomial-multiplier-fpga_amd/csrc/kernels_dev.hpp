@@ -97,6 +97,11 @@
 //   NTTMUL_HOOK_COLS_LD(base, p, sh, col, dir) column passes (dir 0 forward, 1 inverse): word
 //                                           offset their loads start from
 //   NTTMUL_HOOK_COLS_ST(base, p, sh, col)   column passes: word offset of the intermediates' stores
+#if defined(NTTMUL_HOOK_ROWS_LD) || defined(NTTMUL_HOOK_ROWS_ST)
+#define NTTMUL_ROWS_HOOKED 1  // (kbench pricing builds: the row pass keeps global addressing)
+#else
+#define NTTMUL_ROWS_HOOKED 0
+#endif
 #ifndef NTTMUL_HOOK_ROWS_LD
 #define NTTMUL_HOOK_ROWS_LD(base, u, N, b0) (base)
 #endif
@@ -117,6 +122,11 @@
 #endif
 #ifndef NTTMUL_HOOK_XCHG
 #define NTTMUL_HOOK_XCHG() do { } while (0)
+#endif
+#if defined(NTTMUL_HOOK_COLS_LD) || defined(NTTMUL_HOOK_COLS_ST)
+#define NTTMUL_COLS_HOOKED 1  // (kbench pricing builds: the column passes keep global addressing)
+#else
+#define NTTMUL_COLS_HOOKED 0
 #endif
 #ifndef NTTMUL_HOOK_COLS_LD
 #define NTTMUL_HOOK_COLS_LD(base, p, sh, col, dir) (base)
@@ -336,6 +346,26 @@ __device__ __forceinline__ void buf_st32(R r, int byte_off, uint32_t v, int soff
 }
 #ifndef NTTMUL_BUF_SOFF
 #define NTTMUL_BUF_SOFF 1
+#endif
+template <int AUX, class R>
+__device__ __forceinline__ uint64_t buf_ld64(R r, int byte_off, int soff) {
+  typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+  const u2 v = __builtin_amdgcn_raw_buffer_load_b64(r, byte_off, soff, AUX);
+  return ((uint64_t)v.y << 32) | v.x;
+}
+template <int AUX, class R>
+__device__ __forceinline__ void buf_st64(R r, int byte_off, uint64_t v, int soff) {
+  typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+  const u2 w = {(unsigned)v, (unsigned)(v >> 32)};
+  __builtin_amdgcn_raw_buffer_store_b64(w, r, byte_off, soff, AUX);
+}
+// The square split's column passes (k_cols8, 64-bit words) through buffer instructions on a
+// descriptor per polynomial (block-uniform) with 32-bit lane offsets and each register's constant
+// offset in the scalar offset, instead of a 64-bit address per register (NTTMUL_C5_BUF; with the
+// row pass in the same form: C5 1.221 vs 1.243 ms, kbench A/B interleaved, identical checksums,
+// profiles/r6/ab_c5_buf.json)
+#ifndef NTTMUL_C5_BUF
+#define NTTMUL_C5_BUF 1
 #endif
 
 // One forward CT stage l of group g on NPOLY (1 or 2) polynomials (same twiddles); the twiddles
@@ -813,6 +843,12 @@ __global__ __launch_bounds__(rows_threads(LOGS), rows_min_waves(LOGS)) void k_ro
   const size_t base_l = live ? base_g : (size_t)Gr::base(0, j);
   const size_t base_r = NTTMUL_HOOK_ROWS_LD(base_l, u, N, Gr::base(0, j));
 
+  // NTTMUL_C5_BUF, the square split's row pass: one descriptor per polynomial (its 16 rows per
+  // block share it), 32-bit lane offsets, each register's constant offset in the scalar offset
+  constexpr bool kRowBuf = kTile && NTTMUL_C5_BUF && !NTTMUL_ROWS_HOOKED && sizeof(W) == 8 &&
+                           sizeof(TIn) == 8 && sizeof(TOut) == 8 && !kNT;
+  const size_t rpoly = (((size_t)blockIdx.x * PB) >> 8) << 16;  // block-uniform
+  const int rlane = (int)(((u & 255) << 4) + Gr::base(0, j));
   CLK_STAMP(0);
   if constexpr (PRIO) NTTMUL_HOOK_PRIO0(u);  // rows_prio
   W x[16], y[16];
@@ -849,6 +885,15 @@ __global__ __launch_bounds__(rows_threads(LOGS), rows_min_waves(LOGS)) void k_ro
         }
       }
     }
+  } else if constexpr (kRowBuf) {
+    // (units is a multiple of 256 rows here, so every row of the block is live)
+    const auto ra = span_rsrc(a + rpoly, 65536), rb = span_rsrc(b + rpoly, 65536);
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const int so = Gr::off(0, k) * kRS * 8;
+      x[k] = (W)buf_ld64<0>(ra, rlane * 8, so);
+      y[k] = (W)buf_ld64<0>(rb, rlane * 8, so);
+    }
   } else {
 #pragma unroll
     for (int k = 0; k < 16; k++) {
@@ -884,6 +929,13 @@ __global__ __launch_bounds__(rows_threads(LOGS), rows_min_waves(LOGS)) void k_ro
           buf_st32<kAuxSt>(rc, (Gr::base(0, j) + Gr::off(0, k)) * 4, (uint32_t)v);
       }
     }
+    CLK_STAMP(1);
+    return;
+  }
+  if constexpr (kRowBuf) {
+    const auto rc = span_rsrc(c + rpoly, 65536);
+#pragma unroll
+    for (int k = 0; k < 16; k++) buf_st64<0>(rc, rlane * 8, (uint64_t)x[k], Gr::off(0, k) * kRS * 8);
     CLK_STAMP(1);
     return;
   }
@@ -1521,15 +1573,44 @@ __global__ __launch_bounds__(256) void k_cols8(KParams<A> P, const TIn *__restri
   constexpr int kIS = kTile ? 4 : 8;  // log2 word stride of m on the intermediate side
   const size_t base_r = NTTMUL_HOOK_COLS_LD(DIR == 0 ? base : ibase, p, 16, ((g & 15) << 4) + cl, DIR);
   W x[16], y[16];
+  // NTTMUL_C5_BUF: one descriptor per polynomial (p is block-uniform), lane offsets relative to
+  // it (< 512 KiB), each register's constant offset as the scalar offset
+  constexpr bool kBuf = NTTMUL_C5_BUF && !NTTMUL_COLS_HOOKED && sizeof(TIn) == 8 &&
+                        sizeof(TOut) == 8 && NTTMUL_NT_COLS;
+  constexpr int kAuxB = 2;  // nt
+  const size_t pbase = p << 16;
+  if constexpr (kBuf) {
+    const auto ra = span_rsrc(a + pbase, 65536), rb = span_rsrc(b + pbase, 65536);
+    const int lane = (int)((DIR == 0 ? base : ibase) - pbase) +
+                     (Gr::base(GIN, jj) << (DIR == 0 ? 8 : kIS));
 #pragma unroll
-  for (int k = 0; k < 16; k++) {
-    const size_t o = (size_t)(Gr::base(GIN, jj) + Gr::off(GIN, k)) << (DIR == 0 ? 8 : kIS);
-    x[k] = (W)ld_stream<NTTMUL_NT_COLS>(a + base_r + o);
-    y[k] = NPOLY == 2 ? (W)ld_stream<NTTMUL_NT_COLS>(b + base_r + o) : W(0);
+    for (int k = 0; k < 16; k++) {
+      const int so = (Gr::off(GIN, k) << (DIR == 0 ? 8 : kIS)) * 8;
+      x[k] = (W)buf_ld64<kAuxB>(ra, lane * 8, so);
+      y[k] = NPOLY == 2 ? (W)buf_ld64<kAuxB>(rb, lane * 8, so) : W(0);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const size_t o = (size_t)(Gr::base(GIN, jj) + Gr::off(GIN, k)) << (DIR == 0 ? 8 : kIS);
+      x[k] = (W)ld_stream<NTTMUL_NT_COLS>(a + base_r + o);
+      y[k] = NPOLY == 2 ? (W)ld_stream<NTTMUL_NT_COLS>(b + base_r + o) : W(0);
+    }
   }
   if constexpr (DIR == 0) {
     TwPair<W> zw[16];
     fwd_all<A, 8, 0, NPOLY, 0, 0, CW>(P.ar, x, y, lds + cl, lds + cl, P.fw, jj, 0, 0, zw);
+    if constexpr (kBuf) {
+      const auto rta = span_rsrc(ta + pbase, 65536), rtb = span_rsrc(tb + pbase, 65536);
+      const int lane = (int)(ibase - pbase) + (Gr::base(GOUT, jj) << kIS);
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        const int so = (Gr::off(GOUT, k) << kIS) * 8;
+        buf_st64<kAuxB>(rta, lane * 8, (uint64_t)x[k], so);
+        if (NPOLY == 2) buf_st64<kAuxB>(rtb, lane * 8, (uint64_t)y[k], so);
+      }
+      return;
+    }
     const size_t base_w = NTTMUL_HOOK_COLS_ST(ibase, p, 16, ((g & 15) << 4) + cl);
 #pragma unroll
     for (int k = 0; k < 16; k++) {
@@ -1539,6 +1620,15 @@ __global__ __launch_bounds__(256) void k_cols8(KParams<A> P, const TIn *__restri
     }
   } else {
     inv_all<A, 8, G - 1, true, 0, 0, 1, CW>(P, x, y, lds + cl, lds + cl, P.iw, jj, 0, 0);
+    if constexpr (kBuf) {
+      const auto rc = span_rsrc(ta + pbase, 65536);
+      const int lane = (int)(base - pbase) + (Gr::base(GOUT, jj) << 8);
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        buf_st64<kAuxB>(rc, lane * 8, (uint64_t)(A::kInvCanonical ? x[k] : P.ar.canon_inv(x[k])),
+                        (Gr::off(GOUT, k) << 8) * 8);
+      return;
+    }
 #pragma unroll
     for (int k = 0; k < 16; k++) {
       const size_t o = (size_t)(Gr::base(GOUT, jj) + Gr::off(GOUT, k)) << 8;
