@@ -854,8 +854,9 @@ __global__ __launch_bounds__(rows_threads(LOGS), rows_min_waves(LOGS)) void k_ro
   W x[16], y[16];
   // NTTMUL_CPOL >= 0: a, b, c of a one-product-per-block u32 product through buffer loads /
   // stores (descriptor from block-uniform values, 32-bit per-lane offsets, nt by default)
-  // (64-bit words and the multi-pass passes keep global loads: the same form measured +0.8 % at
-  // C5, its row pass at 131 VGPRs instead of 126)
+  // (64-bit words of the square split take kRowBuf below: one descriptor per polynomial and the
+  // constant offsets in the scalar offset; round 2's form, an offset per register, measured
+  // +0.8 % at C5 with its row pass at 131 VGPRs instead of 126)
   constexpr bool kCpol = NTTMUL_CPOL >= 0 && PB == 1 && L1 == 0 && sizeof(W) == 4 &&
                          sizeof(TIn) == 4 && sizeof(TOut) == 4;
   constexpr int kAux = NTTMUL_CPOL < 0 ? 0 : NTTMUL_CPOL;
