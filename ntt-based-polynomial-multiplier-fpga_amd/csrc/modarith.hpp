@@ -628,10 +628,12 @@ struct Arith32W {
 #define NTTMUL_A64_V2 1
 #endif
 // base multiplication sums from 31-bit limb products (Arith64::basemul): -3.6 % VALU in the C5
-// row pass (the 128-bit carries and moves go; the 16 multiply-adds per output stay) but C5 time
-// unchanged at the power cap (profiles/r2/c5_limb_ab.txt, identical checksums): off
+// row pass (the 128-bit carries and moves go; the 16 multiply-adds per output stay).  C5 time
+// unchanged at the power cap in round 2 (profiles/r2/c5_limb_ab.txt), +0.5 % in round 5
+// (profiles/r5/c5_limb/); on round 6's buffer-addressed row pass -0.45 % and -0.36 % in two
+// kbench sessions (profiles/r6/ab_c5_limb*.json, identical checksums, same board power): on
 #ifndef NTTMUL_A64_LIMB
-#define NTTMUL_A64_LIMB 0
+#define NTTMUL_A64_LIMB 1
 #endif
 // high product through the carry-out of v_mad_u64_u32 (Arith64::mulhi64; tools/kbench A/B)
 #ifndef NTTMUL_A64_MADC
